@@ -1,0 +1,199 @@
+"""ctypes binding of oracle/liboracle.so (the C restatement).  TEST INFRASTRUCTURE ONLY:
+imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product path (ringo-snark_amd/)."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so not built (run `make -C oracle`)")
+        _LIB = ctypes.CDLL(path)
+        L = _LIB
+        L.of_field_size.restype = ctypes.c_size_t
+        L.of_primitive_root.restype = ctypes.c_uint64
+        L.of_primitive_root.argtypes = [ctypes.c_uint64]
+        L.of_lattigo_psi.restype = ctypes.c_uint64
+        L.of_lattigo_psi.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        L.of_jindo_create.restype = ctypes.c_void_p
+        L.of_jindo_create.argtypes = [ctypes.c_void_p]
+        L.of_jindo_destroy.argtypes = [ctypes.c_void_p]
+        L.of_ntt_fwd.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
+        L.of_ntt_inv.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
+        L.of_vec.argtypes = [ctypes.c_void_p, ctypes.c_int, u64p, u64p, u64p, ctypes.c_long]
+    return _LIB
+
+
+def ptr(a, t=u64p):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def to_limbs(values, L):
+    """list of ints -> np.uint64 [n, L] little-endian limbs"""
+    out = np.zeros((len(values), L), dtype=np.uint64)
+    m = (1 << 64) - 1
+    for i, v in enumerate(values):
+        for j in range(L):
+            out[i, j] = (v >> (64 * j)) & m
+    return out
+
+
+def from_limbs(arr):
+    arr = np.asarray(arr, dtype=np.uint64).reshape(-1, arr.shape[-1])
+    L = arr.shape[1]
+    return [sum(int(arr[i, j]) << (64 * j) for j in range(L)) for i in range(arr.shape[0])]
+
+
+class CField:
+    def __init__(self, q, L=None):
+        self.q = q
+        self.L = L or (q.bit_length() + 63) // 64
+        self.buf = ctypes.create_string_buffer(lib().of_field_size())
+        ql = to_limbs([q], self.L)[0]
+        rc = lib().of_field_init(self.buf, self.L, ptr(ql))
+        if rc:
+            raise ValueError("bad field")
+
+    def consts(self):
+        qinv = ctypes.c_uint64()
+        r2 = np.zeros(self.L, np.uint64)
+        one = np.zeros(self.L, np.uint64)
+        lib().of_field_consts(self.buf, ctypes.byref(qinv), ptr(r2), ptr(one))
+        return qinv.value, from_limbs(r2[None, :])[0], from_limbs(one[None, :])[0]
+
+    def _bin(self, fn, x, y=None):
+        z = np.zeros(self.L, np.uint64)
+        xa = to_limbs([x], self.L)[0]
+        if y is None:
+            getattr(lib(), fn)(self.buf, ptr(z), ptr(xa))
+        else:
+            ya = to_limbs([y], self.L)[0]
+            getattr(lib(), fn)(self.buf, ptr(z), ptr(xa), ptr(ya))
+        return from_limbs(z[None, :])[0]
+
+    def mul(self, x, y):
+        return self._bin("of_f_mul", x, y)
+
+    def add(self, x, y):
+        return self._bin("of_f_add", x, y)
+
+    def sub(self, x, y):
+        return self._bin("of_f_sub", x, y)
+
+    def neg(self, x):
+        return self._bin("of_f_neg", x)
+
+    def tables(self, N, cyclic=False):
+        """(tw [N,L], twinv [N,L], ninv [L]) as np.uint64 (Montgomery), or raises."""
+        tw = np.zeros((N, self.L), np.uint64)
+        twi = np.zeros((N, self.L), np.uint64)
+        ninv = np.zeros(self.L, np.uint64)
+        fn = lib().of_cyclic_tables if cyclic else lib().of_cyclotomic_tables
+        rc = fn(self.buf, N, ptr(tw), ptr(twi), ptr(ninv))
+        if rc == -1:
+            raise ValueError("rank must be a power of two")
+        if rc:
+            raise ValueError("NTT not supported")
+        return tw, twi, ninv
+
+    def ntt_fwd(self, a, tw):
+        """a: np.uint64 [batch, N, L] -> new array"""
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        out = np.empty_like(a)
+        lib().of_ntt_fwd(self.buf, ptr(out), ptr(a), ptr(np.ascontiguousarray(tw)), a.shape[-2],
+                         a.size // (a.shape[-2] * self.L))
+        return out
+
+    def ntt_inv(self, a, twi, ninv):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        out = np.empty_like(a)
+        lib().of_ntt_inv(self.buf, ptr(out), ptr(a), ptr(np.ascontiguousarray(twi)), ptr(np.ascontiguousarray(ninv)),
+                         a.shape[-2], a.size // (a.shape[-2] * self.L))
+        return out
+
+    VEC_OPS = {"add": 0, "sub": 1, "neg": 2, "mul": 3, "smul": 4, "mul_add": 5, "mul_sub": 6,
+               "smul_add": 7, "smul_sub": 8}
+
+    def vec(self, op, out, a, b=None):
+        """in-place on `out` (np.uint64 [n, L]); matches rg_vec semantics."""
+        n = out.size // self.L
+        lib().of_vec(self.buf, self.VEC_OPS[op], ptr(out), ptr(a), ptr(b), n)
+        return out
+
+
+class OfJindoParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ["rank", "rows", "cols", "slots", "exp", "d", "in_msis", "out_msis", "mlwe", "dcmp",
+                 "log_in_cut", "log_out_cut"]] + [
+        ("base", ctypes.c_uint64), ("nq", ctypes.c_int), ("nqo", ctypes.c_int),
+        ("q", ctypes.c_uint64 * 4), ("qo", ctypes.c_uint64 * 4), ("field_limbs", ctypes.c_int),
+        ("field_q", ctypes.c_uint64 * 16)]
+
+
+def make_params_struct(P, field_q, cls=OfJindoParams):
+    s = cls()
+    for k, a in [("rank", "rank"), ("rows", "rows"), ("cols", "cols"), ("slots", "slots"), ("exp", "exp"),
+                 ("d", "d"), ("in_msis", "in_msis"), ("out_msis", "out_msis"), ("mlwe", "mlwe"),
+                 ("dcmp", "in_com_dcmp_len"), ("log_in_cut", "log_in_cut"), ("log_out_cut", "log_out_cut")]:
+        setattr(s, k, int(P[a] if isinstance(P, dict) else getattr(P, a)))
+    g = (lambda k: P[k]) if isinstance(P, dict) else (lambda k: getattr(P, k))
+    s.base = g("base")
+    q, qo = list(g("q")), list(g("qo"))
+    s.nq, s.nqo = len(q), len(qo)
+    for i, x in enumerate(q):
+        s.q[i] = x
+    for i, x in enumerate(qo):
+        s.qo[i] = x
+    L = (field_q.bit_length() + 63) // 64
+    s.field_limbs = L
+    for i in range(L):
+        s.field_q[i] = (field_q >> (64 * i)) & ((1 << 64) - 1)
+    return s
+
+
+class CJindo:
+    """C-oracle commit with injected randomness (same layouts as rg_jindo_commit)."""
+
+    def __init__(self, P, field_q):
+        self.P = P
+        self.ps = make_params_struct(P, field_q)
+        self.h = lib().of_jindo_create(ctypes.byref(self.ps))
+        if not self.h:
+            raise ValueError("bad jindo params")
+        self.L = self.ps.field_limbs
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().of_jindo_destroy(self.h)
+            self.h = None
+
+    def shapes(self):
+        s = self.ps
+        nm = s.in_msis + s.mlwe
+        return dict(incom=(s.dcmp, s.nqo, s.d), enc=(s.cols + 1, s.rows, s.nq, s.d),
+                    mlwe=(s.cols + 1, nm, s.nq, s.d), com=(s.out_msis, s.nq, s.d))
+
+    def commit(self, ck_in, ck_mlwe, ck_out, v, last_row, mask, enc_noise, mlwe_noise):
+        sh = self.shapes()
+        o = {k: np.zeros(v_, np.uint64) for k, v_ in sh.items()}
+        args = [np.ascontiguousarray(x) for x in (ck_in, ck_mlwe, ck_out, v, last_row, mask)]
+        en = np.ascontiguousarray(enc_noise, dtype=np.int64)
+        mn = np.ascontiguousarray(mlwe_noise, dtype=np.int64)
+        rc = lib().of_jindo_commit(
+            ctypes.c_void_p(self.h), ptr(args[0]), ptr(args[1]), ptr(args[2]), ptr(args[3]),
+            ctypes.c_long(args[3].shape[0]), ptr(args[4]), ptr(args[5]), ptr(en, i64p), ptr(mn, i64p),
+            ptr(o["incom"]), ptr(o["enc"]), ptr(o["mlwe"]), ptr(o["com"]))
+        if rc:
+            raise ValueError("len(v) > params.rank")
+        return o

@@ -1,0 +1,773 @@
+/* oracle.c -- CPU restatement of the ringo-snark hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the checker (and bench.py's timed "port" CPU baseline), never the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load liboracle.so.
+ * It is a plain-C restatement of the reference's algorithms, cross-checked against the
+ * big-int restatement oracle/pyref.py and the reference's generated field constants
+ * (tests/golden/fields.json).  File:line citations are into sp301415/ringo-snark.
+ *
+ *   field      jindo/internal/zp/element.go:397-466 (Add/Sub/Neg), element_purego.go:46-213 (Mul)
+ *   bigpoly    math/bigpoly/ntt.go:153-203 (tables), :246-466 (transforms), vec.go:9-121
+ *   jindo      jindo/encoder.go:120-201, jindo/prover.go:45-202, jindo/rns.go:76-114
+ *   lattigo    ring NTT/INTT/MForm/IMForm/MulCoeffsMontgomeryThenAdd (v6.1.0, source absent:
+ *              restated from its published algorithm -- PARITY UNPINNED at that boundary)
+ *
+ * Layouts are identical to the C-ABI in include/ringo.h so tests compare buffers bytewise.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+#define MAXL 16
+
+typedef struct {
+  int L;
+  uint64_t q[MAXL];
+  uint64_t qinv; /* -q^-1 mod 2^64  (element.go:70-72) */
+  uint64_t r2[MAXL];
+  uint64_t one[MAXL]; /* R mod q */
+} of_field;
+
+/* ------------------------------------------------------------------------------------------ */
+/* multi-limb helpers                                                                          */
+/* ------------------------------------------------------------------------------------------ */
+static inline int geq(const uint64_t* a, const uint64_t* b, int L) {
+  for (int i = L - 1; i >= 0; --i) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return 1;
+}
+static inline uint64_t add_n(uint64_t* z, const uint64_t* a, const uint64_t* b, int L) {
+  uint64_t c = 0;
+  for (int i = 0; i < L; ++i) {
+    u128 s = (u128)a[i] + b[i] + c;
+    z[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  return c;
+}
+static inline uint64_t sub_n(uint64_t* z, const uint64_t* a, const uint64_t* b, int L) {
+  uint64_t br = 0;
+  for (int i = 0; i < L; ++i) {
+    u128 d = (u128)a[i] - b[i] - br;
+    z[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  return br;
+}
+
+/* Add: z = x + y, conditional -q (element.go:397-413) */
+static inline void f_add(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y, int L) {
+  uint64_t t[MAXL];
+  uint64_t c = add_n(t, x, y, L);
+  if (c || geq(t, F->q, L)) sub_n(t, t, F->q, L);
+  memcpy(z, t, 8 * L);
+}
+/* Sub: z = x - y, conditional +q (element.go:437-451) */
+static inline void f_sub(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y, int L) {
+  uint64_t t[MAXL];
+  if (sub_n(t, x, y, L)) add_n(t, t, F->q, L);
+  memcpy(z, t, 8 * L);
+}
+/* Neg: 0 -> 0, else q - x (element.go:454-466) */
+static inline void f_neg(const of_field* F, uint64_t* z, const uint64_t* x, int L) {
+  int zero = 1;
+  for (int i = 0; i < L; ++i) zero &= x[i] == 0;
+  if (zero) {
+    memset(z, 0, 8 * L);
+    return;
+  }
+  sub_n(z, F->q, x, L);
+}
+/* Montgomery CIOS z = x*y*R^-1 mod q, fully reduced (element_purego.go:46-213). */
+static inline void f_mul(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y, int L) {
+  uint64_t t[MAXL + 2];
+  memset(t, 0, sizeof(uint64_t) * (L + 2));
+  for (int i = 0; i < L; ++i) {
+    uint64_t c = 0;
+    for (int j = 0; j < L; ++j) {
+      u128 s = (u128)x[i] * y[j] + t[j] + c;
+      t[j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    u128 s = (u128)t[L] + c;
+    t[L] = (uint64_t)s;
+    t[L + 1] = (uint64_t)(s >> 64);
+    uint64_t m = t[0] * F->qinv;
+    s = (u128)m * F->q[0] + t[0];
+    c = (uint64_t)(s >> 64);
+    for (int j = 1; j < L; ++j) {
+      s = (u128)m * F->q[j] + t[j] + c;
+      t[j - 1] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    s = (u128)t[L] + c;
+    t[L - 1] = (uint64_t)s;
+    t[L] = t[L + 1] + (uint64_t)(s >> 64);
+  }
+  if (t[L] || geq(t, F->q, L)) sub_n(t, t, F->q, L);
+  memcpy(z, t, 8 * L);
+}
+
+int of_field_init(of_field* F, int L, const uint64_t* q) {
+  if (L < 1 || L > MAXL || !(q[0] & 1)) return -1;
+  memset(F, 0, sizeof(*F));
+  F->L = L;
+  memcpy(F->q, q, 8 * L);
+  uint64_t inv = 1; /* Newton: q^-1 mod 2^64 */
+  for (int i = 0; i < 7; ++i) inv *= 2 - q[0] * inv;
+  F->qinv = 0 - inv;
+  /* R mod q by doubling 1 (64L times); R^2 by doubling (128L times). */
+  uint64_t r[MAXL] = {1};
+  for (int i = 0; i < 128 * L; ++i) {
+    f_add(F, r, r, r, L);
+    if (i == 64 * L - 1) memcpy(F->one, r, 8 * L);
+  }
+  memcpy(F->r2, r, 8 * L);
+  return 0;
+}
+void of_field_consts(const of_field* F, uint64_t* qinv, uint64_t* r2, uint64_t* one) {
+  *qinv = F->qinv;
+  memcpy(r2, F->r2, 8 * F->L);
+  memcpy(one, F->one, 8 * F->L);
+}
+size_t of_field_size(void) { return sizeof(of_field); }
+
+/* exported element ops (for tests) */
+void of_f_mul(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y) { f_mul(F, z, x, y, F->L); }
+void of_f_add(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y) { f_add(F, z, x, y, F->L); }
+void of_f_sub(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* y) { f_sub(F, z, x, y, F->L); }
+void of_f_neg(const of_field* F, uint64_t* z, const uint64_t* x) { f_neg(F, z, x, F->L); }
+
+/* z = x^e (Montgomery), e given as little-endian limbs (ne words) */
+static void f_pow(const of_field* F, uint64_t* z, const uint64_t* x, const uint64_t* e, int ne) {
+  int L = F->L;
+  uint64_t r[MAXL], b[MAXL];
+  memcpy(r, F->one, 8 * L);
+  memcpy(b, x, 8 * L);
+  for (int w = 0; w < ne; ++w)
+    for (int k = 0; k < 64; ++k) {
+      if ((e[w] >> k) & 1) f_mul(F, r, r, b, L);
+      f_mul(F, b, b, b, L);
+    }
+  memcpy(z, r, 8 * L);
+}
+static void f_from_u64(const of_field* F, uint64_t* z, uint64_t v) { /* SetUint64 (element.go:93-97) */
+  uint64_t t[MAXL] = {0};
+  t[0] = v;
+  f_mul(F, z, t, F->r2, F->L);
+}
+static void shr_n(uint64_t* z, const uint64_t* a, int L, int s) { /* s < 64 */
+  for (int i = 0; i < L; ++i) z[i] = (a[i] >> s) | (s && i + 1 < L ? a[i + 1] << (64 - s) : 0);
+}
+static void bitrev_perm(uint64_t* v, int N, int L) { /* vec.go:123-137 */
+  int j = 0;
+  uint64_t tmp[MAXL];
+  for (int i = 1; i < N; ++i) {
+    int bit = N >> 1;
+    for (; j >= bit; bit >>= 1) j -= bit;
+    j += bit;
+    if (i < j) {
+      memcpy(tmp, v + (size_t)i * L, 8 * L);
+      memcpy(v + (size_t)i * L, v + (size_t)j * L, 8 * L);
+      memcpy(v + (size_t)j * L, tmp, 8 * L);
+    }
+  }
+}
+
+/* Generator search (ntt.go:46-53 / :173-180): first x=2,3,.. with (x^t1)^t2 != 1; t1 =
+ * (p-1)/root_order via a right shift (root_order is a power of two dividing p-1). */
+static int find_root(const of_field* F, int log_order, uint64_t t2, uint64_t* g) {
+  int L = F->L;
+  uint64_t pm1[MAXL], t1[MAXL], x[MAXL], gp[MAXL], e2[1] = {t2};
+  memcpy(pm1, F->q, 8 * L);
+  pm1[0] -= 1;
+  memcpy(t1, pm1, 8 * L);
+  for (int s = log_order; s > 0; s -= (s > 63 ? 63 : s)) shr_n(t1, t1, L, s > 63 ? 63 : s);
+  for (uint64_t xv = 2; xv < 1000000; ++xv) {
+    f_from_u64(F, x, xv);
+    f_pow(F, g, x, t1, L);
+    f_pow(F, gp, g, e2, 1);
+    if (memcmp(gp, F->one, 8 * L) != 0) return 0;
+  }
+  return -1;
+}
+static int log2i(uint64_t n) {
+  int k = 0;
+  while ((1ull << k) < n) ++k;
+  return k;
+}
+static int check_support(const of_field* F, int N) {
+  if (N <= 0 || (N & (N - 1))) return -1; /* "rank must be a power of two" */
+  uint64_t pm1 = F->q[0] - 1;           /* 2N | p-1 ("NTT not supported", ntt.go:162-164) */
+  int tz = pm1 ? __builtin_ctzll(pm1) : 64;
+  return (tz >= log2i((uint64_t)N) + 1) ? 0 : -2;
+}
+
+/* NewCyclotomicTransformer (ntt.go:153-203): tw[k] = psi^brv(k), twinv[k] = psi^-brv(k). */
+int of_cyclotomic_tables(const of_field* F, int N, uint64_t* tw, uint64_t* twinv, uint64_t* ninv) {
+  int rc = check_support(F, N), L = F->L;
+  if (rc) return rc;
+  uint64_t g[MAXL], gi[MAXL], pm2[MAXL];
+  if (find_root(F, log2i(N) + 1, (uint64_t)N, g)) return -3;
+  uint64_t two[MAXL] = {2};
+  sub_n(pm2, F->q, two, L);
+  f_pow(F, gi, g, pm2, L);
+  memcpy(tw, F->one, 8 * L);
+  memcpy(twinv, F->one, 8 * L);
+  for (int i = 1; i < N; ++i) {
+    f_mul(F, tw + (size_t)i * L, tw + (size_t)(i - 1) * L, g, L);
+    f_mul(F, twinv + (size_t)i * L, twinv + (size_t)(i - 1) * L, gi, L);
+  }
+  bitrev_perm(tw, N, L);
+  bitrev_perm(twinv, N, L);
+  uint64_t n[MAXL];
+  f_from_u64(F, n, (uint64_t)N);
+  f_pow(F, ninv, n, pm2, L);
+  return 0;
+}
+
+/* NewCyclicTransformer (ntt.go:26-95): per-stage table tw[m+i] = brv_{N/2}(w^j)[i]. */
+int of_cyclic_tables(const of_field* F, int N, uint64_t* tw, uint64_t* twinv, uint64_t* ninv) {
+  int rc = check_support(F, N), L = F->L;
+  if (rc) return rc;
+  uint64_t g[MAXL], gi[MAXL], pm2[MAXL];
+  if (find_root(F, log2i(N), (uint64_t)(N >> 1), g)) return -3;
+  uint64_t two[MAXL] = {2};
+  sub_n(pm2, F->q, two, L);
+  f_pow(F, gi, g, pm2, L);
+  int h = N / 2 > 0 ? N / 2 : 1;
+  uint64_t* ref = (uint64_t*)calloc((size_t)h * L, 8);
+  uint64_t* refi = (uint64_t*)calloc((size_t)h * L, 8);
+  memcpy(ref, F->one, 8 * L);
+  memcpy(refi, F->one, 8 * L);
+  for (int i = 1; i < N / 2; ++i) {
+    f_mul(F, ref + (size_t)i * L, ref + (size_t)(i - 1) * L, g, L);
+    f_mul(F, refi + (size_t)i * L, refi + (size_t)(i - 1) * L, gi, L);
+  }
+  if (N >= 2) {
+    bitrev_perm(ref, N / 2, L);
+    bitrev_perm(refi, N / 2, L);
+  }
+  memset(tw, 0, (size_t)N * L * 8);
+  memset(twinv, 0, (size_t)N * L * 8);
+  for (int m = 1; m <= N / 2; m <<= 1)
+    for (int i = 0; i < m; ++i) {
+      memcpy(tw + (size_t)(m + i) * L, ref + (size_t)i * L, 8 * L);
+      memcpy(twinv + (size_t)(m + i) * L, refi + (size_t)i * L, 8 * L);
+    }
+  free(ref);
+  free(refi);
+  uint64_t n[MAXL];
+  f_from_u64(F, n, (uint64_t)N);
+  f_pow(F, ninv, n, pm2, L);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* bigpoly transforms: nttInPlaceRef / inttInPlaceRef (ntt.go:254-275, 365-386) -- the
+ * unrolled variants (:277-355, :388-466) perform the identical butterflies in another order.  */
+/* ------------------------------------------------------------------------------------------ */
+static inline void ntt_one(const of_field* F, uint64_t* p, const uint64_t* tw, int N, int L) {
+  uint64_t v[MAXL];
+  int t = N;
+  for (int m = 1; m <= N / 2; m <<= 1) {
+    t >>= 1;
+    for (int i = 0; i < m; ++i) {
+      const uint64_t* w = tw + (size_t)(m + i) * L;
+      for (int j = 2 * i * t; j < 2 * i * t + t; ++j) {
+        uint64_t* u = p + (size_t)j * L;
+        uint64_t* x = p + (size_t)(j + t) * L;
+        f_mul(F, v, x, w, L); /* butterfly: v*=w; u+=v; v = u-2v  == (u+v, u-v) */
+        f_sub(F, x, u, v, L);
+        f_add(F, u, u, v, L);
+      }
+    }
+  }
+}
+static inline void intt_one(const of_field* F, uint64_t* p, const uint64_t* twinv, const uint64_t* ninv,
+                            int N, int L) {
+  uint64_t d[MAXL];
+  int t = 1;
+  for (int m = N / 2; m >= 1; m >>= 1) {
+    for (int i = 0; i < m; ++i) {
+      const uint64_t* w = twinv + (size_t)(m + i) * L;
+      for (int j = 2 * i * t; j < 2 * i * t + t; ++j) {
+        uint64_t* u = p + (size_t)j * L;
+        uint64_t* x = p + (size_t)(j + t) * L;
+        f_sub(F, d, u, x, L);
+        f_add(F, u, u, x, L);
+        f_mul(F, x, d, w, L);
+      }
+    }
+    t <<= 1;
+  }
+  for (int j = 0; j < N; ++j) f_mul(F, p + (size_t)j * L, p + (size_t)j * L, ninv, L);
+}
+
+#define DISPATCH_L(L, CALL)   \
+  switch (L) {                \
+    case 1: { enum { LL = 1 }; CALL; } break;  \
+    case 2: { enum { LL = 2 }; CALL; } break;  \
+    case 4: { enum { LL = 4 }; CALL; } break;  \
+    case 7: { enum { LL = 7 }; CALL; } break;  \
+    case 14: { enum { LL = 14 }; CALL; } break; \
+    default: { const int LL = L; CALL; } break; \
+  }
+
+/* in/out: [batch][N][L]; out may alias in (the Go side copies first, ntt.go:206-222). */
+void of_ntt_fwd(const of_field* F, uint64_t* out, const uint64_t* in, const uint64_t* tw, int N, long batch) {
+  if (out != in) memcpy(out, in, (size_t)batch * N * F->L * 8);
+#pragma omp parallel for schedule(static)
+  for (long b = 0; b < batch; ++b) DISPATCH_L(F->L, ntt_one(F, out + (size_t)b * N * LL, tw, N, LL));
+}
+void of_ntt_inv(const of_field* F, uint64_t* out, const uint64_t* in, const uint64_t* twinv,
+                const uint64_t* ninv, int N, long batch) {
+  if (out != in) memcpy(out, in, (size_t)batch * N * F->L * 8);
+#pragma omp parallel for schedule(static)
+  for (long b = 0; b < batch; ++b) DISPATCH_L(F->L, intt_one(F, out + (size_t)b * N * LL, twinv, ninv, N, LL));
+}
+
+/* pointwise ops (vec.go:9-121, base_op.go:49-171).  op codes match include/ringo.h rg_vec_op. */
+enum { OV_ADD = 0, OV_SUB, OV_NEG, OV_MUL, OV_SMUL, OV_MUL_ADD, OV_MUL_SUB, OV_SMUL_ADD, OV_SMUL_SUB };
+void of_vec(const of_field* F, int op, uint64_t* out, const uint64_t* a, const uint64_t* b, long n) {
+  int L = F->L;
+  uint64_t t[MAXL];
+  for (long i = 0; i < n; ++i) {
+    uint64_t* z = out + (size_t)i * L;
+    const uint64_t* x = a + (size_t)i * L;
+    const uint64_t* y = (op == OV_SMUL || op == OV_SMUL_ADD || op == OV_SMUL_SUB) ? b : (b ? b + (size_t)i * L : 0);
+    switch (op) {
+      case OV_ADD: f_add(F, z, x, y, L); break;
+      case OV_SUB: f_sub(F, z, x, y, L); break;
+      case OV_NEG: f_neg(F, z, x, L); break;
+      case OV_MUL: case OV_SMUL: f_mul(F, z, x, y, L); break;
+      case OV_MUL_ADD: case OV_SMUL_ADD: f_mul(F, t, x, y, L); f_add(F, z, z, t, L); break;
+      case OV_MUL_SUB: case OV_SMUL_SUB: f_mul(F, t, x, y, L); f_sub(F, z, z, t, L); break;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Lattigo-convention word ring (d-point negacyclic, per prime)                                 */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)((u128)a * b % q); }
+static uint64_t powmod(uint64_t a, uint64_t e, uint64_t q) {
+  uint64_t r = 1 % q;
+  a %= q;
+  while (e) {
+    if (e & 1) r = mulmod(r, a, q);
+    a = mulmod(a, a, q);
+    e >>= 1;
+  }
+  return r;
+}
+static int is_prime_u64(uint64_t n) {
+  if (n < 2) return 0;
+  static const uint64_t sp[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  for (int i = 0; i < 12; ++i)
+    if (n % sp[i] == 0) return n == sp[i];
+  uint64_t d = n - 1;
+  int r = 0;
+  while (!(d & 1)) d >>= 1, ++r;
+  for (int i = 0; i < 12; ++i) {
+    uint64_t x = powmod(sp[i], d, n);
+    if (x == 1 || x == n - 1) continue;
+    int ok = 0;
+    for (int k = 1; k < r; ++k) {
+      x = mulmod(x, x, n);
+      if (x == n - 1) { ok = 1; break; }
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+static uint64_t gcd_u64(uint64_t a, uint64_t b) {
+  while (b) { uint64_t t = a % b; a = b; b = t; }
+  return a;
+}
+static uint64_t rho(uint64_t n) {
+  if (!(n & 1)) return 2;
+  for (uint64_t c = 1;; ++c) {
+    uint64_t x = 2, y = 2, d = 1;
+    while (d == 1) {
+      x = (mulmod(x, x, n) + c) % n;
+      y = (mulmod(y, y, n) + c) % n;
+      y = (mulmod(y, y, n) + c) % n;
+      d = gcd_u64(x > y ? x - y : y - x, n);
+    }
+    if (d != n) return d;
+  }
+}
+static int factor_rec(uint64_t n, uint64_t* f, int nf) {
+  if (n == 1) return nf;
+  if (is_prime_u64(n)) {
+    for (int i = 0; i < nf; ++i) if (f[i] == n) return nf;
+    f[nf] = n;
+    return nf + 1;
+  }
+  uint64_t d = rho(n);
+  nf = factor_rec(d, f, nf);
+  return factor_rec(n / d, f, nf);
+}
+/* ring.PrimitiveRoot: smallest g >= 3 that is a primitive root mod q. */
+uint64_t of_primitive_root(uint64_t q) {
+  uint64_t f[64];
+  int nf = factor_rec(q - 1, f, 0);
+  for (uint64_t g = 3;; ++g) {
+    int ok = 1;
+    for (int i = 0; i < nf && ok; ++i) ok = powmod(g, (q - 1) / f[i], q) != 1;
+    if (ok) return g;
+  }
+}
+static uint64_t brv(uint64_t x, int logn) {
+  uint64_t r = 0;
+  for (int i = 0; i < logn; ++i) r = (r << 1) | ((x >> i) & 1);
+  return r;
+}
+typedef struct {
+  uint64_t q;
+  int d, logd;
+  uint64_t* roots;   /* plain residues, roots[brv(j)] = psi^j */
+  uint64_t* iroots;
+  uint64_t ninv, m, minv; /* 2^64 mod q, 2^-64 mod q */
+} of_subring;
+static void subring_init(of_subring* S, int d, uint64_t q) {
+  S->q = q;
+  S->d = d;
+  S->logd = log2i((uint64_t)d);
+  uint64_t g = of_primitive_root(q);
+  uint64_t psi = powmod(g, (q - 1) / (2 * (uint64_t)d), q), psii = powmod(psi, q - 2, q);
+  S->roots = (uint64_t*)malloc(8 * (size_t)d);
+  S->iroots = (uint64_t*)malloc(8 * (size_t)d);
+  uint64_t a = 1, b = 1;
+  for (int j = 0; j < d; ++j) {
+    S->roots[brv((uint64_t)j, S->logd)] = a;
+    S->iroots[brv((uint64_t)j, S->logd)] = b;
+    a = mulmod(a, psi, q);
+    b = mulmod(b, psii, q);
+  }
+  S->ninv = powmod((uint64_t)d, q - 2, q);
+  S->m = (uint64_t)(((u128)1 << 64) % q);
+  S->minv = powmod(S->m, q - 2, q);
+}
+static void subring_free(of_subring* S) {
+  free(S->roots);
+  free(S->iroots);
+}
+uint64_t of_lattigo_psi(uint64_t q, int d) {
+  return powmod(of_primitive_root(q), (q - 1) / (2 * (uint64_t)d), q);
+}
+static void r_ntt(const of_subring* S, uint64_t* p) {
+  uint64_t q = S->q;
+  int N = S->d, t = N;
+  for (int m = 1; m < N; m <<= 1) {
+    t >>= 1;
+    for (int i = 0; i < m; ++i) {
+      uint64_t w = S->roots[m + i];
+      for (int j = 2 * i * t; j < 2 * i * t + t; ++j) {
+        uint64_t u = p[j], v = mulmod(p[j + t], w, q);
+        p[j] = u + v >= q ? u + v - q : u + v;
+        p[j + t] = u >= v ? u - v : u + q - v;
+      }
+    }
+  }
+}
+static void r_intt(const of_subring* S, uint64_t* p) {
+  uint64_t q = S->q;
+  int N = S->d, t = 1;
+  for (int m = N / 2; m >= 1; m >>= 1) {
+    for (int i = 0; i < m; ++i) {
+      uint64_t w = S->iroots[m + i];
+      for (int j = 2 * i * t; j < 2 * i * t + t; ++j) {
+        uint64_t u = p[j], v = p[j + t];
+        p[j] = u + v >= q ? u + v - q : u + v;
+        p[j + t] = mulmod(u >= v ? u - v : u + q - v, w, q);
+      }
+    }
+    t <<= 1;
+  }
+  for (int j = 0; j < N; ++j) p[j] = mulmod(p[j], S->ninv, q);
+}
+static inline uint64_t signed_res(int64_t c, uint64_t q) { /* setCoeffSigned (utils.go:49-61) */
+  if (c >= 0) return (uint64_t)c;
+  uint64_t a = (uint64_t)(-(c + 1)) + 1; /* |c| */
+  return q - a % q;                      /* Go: c%q + q  (== q when q | c) */
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Jindo commit with injected randomness (layouts: include/ringo.h rg_jindo_commit)            */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int rank, rows, cols, slots, exp, d, in_msis, out_msis, mlwe, dcmp, log_in_cut, log_out_cut;
+  uint64_t base;
+  int nq, nqo;
+  uint64_t q[4], qo[4];
+  int field_limbs;
+  uint64_t field_q[MAXL];
+} of_jindo_params;
+
+typedef struct {
+  of_jindo_params P;
+  of_field F;
+  of_subring rq[4], ro[4];
+} of_jindo;
+
+of_jindo* of_jindo_create(const of_jindo_params* P) {
+  if (P->nq < 1 || P->nq > 4 || P->nqo < 1 || P->nqo > 4 || P->nqo > P->nq) return 0;
+  of_jindo* J = (of_jindo*)calloc(1, sizeof(of_jindo));
+  J->P = *P;
+  if (of_field_init(&J->F, P->field_limbs, P->field_q)) { free(J); return 0; }
+  for (int l = 0; l < P->nq; ++l) subring_init(&J->rq[l], P->d, P->q[l]);
+  for (int l = 0; l < P->nqo; ++l) subring_init(&J->ro[l], P->d, P->qo[l]);
+  return J;
+}
+void of_jindo_destroy(of_jindo* J) {
+  for (int l = 0; l < J->P.nq; ++l) subring_free(&J->rq[l]);
+  for (int l = 0; l < J->P.nqo; ++l) subring_free(&J->ro[l]);
+  free(J);
+}
+
+/* baseEncodeTo (encoder.go:120-146): digits[d] from n<=slots Montgomery elements. */
+static void base_encode(const of_jindo* J, uint64_t* digits, const uint64_t* v, int n) {
+  const of_jindo_params* P = &J->P;
+  int L = J->F.L;
+  memset(digits, 0, 8 * (size_t)P->d);
+  uint64_t one[MAXL] = {1}, c[MAXL];
+  for (int i = 0; i < n; ++i) {
+    f_mul(&J->F, c, v + (size_t)i * L, one, L); /* Slice = fromMont (element.go:1769-1773) */
+    for (int j = 0; j < P->exp - 1; ++j) {       /* divMod64 (utils.go:12-19) */
+      uint64_t r = 0;
+      for (int k = L - 1; k >= 0; --k) {
+        u128 num = ((u128)r << 64) | c[k];
+        c[k] = (uint64_t)(num / P->base);
+        r = (uint64_t)(num % P->base);
+      }
+      digits[j * P->slots + i] = r;
+    }
+    digits[(P->exp - 1) * P->slots + i] = c[0];
+  }
+}
+/* randEncodeTo tail (encoder.go:166-200) with injected samples; out: [nq][d]. */
+static void rand_encode(const of_jindo* J, uint64_t* out, const uint64_t* v, int n, const int64_t* noise) {
+  const of_jindo_params* P = &J->P;
+  int d = P->d, sl = P->slots;
+  uint64_t* digits = (uint64_t*)malloc(8 * (size_t)d);
+  uint64_t* s = (uint64_t*)malloc(8 * (size_t)d);
+  uint64_t* sh = (uint64_t*)malloc(8 * (size_t)d);
+  base_encode(J, digits, v, n);
+  for (int l = 0; l < P->nq; ++l) {
+    const of_subring* S = &J->rq[l];
+    uint64_t q = S->q;
+    for (int i = 0; i < d; ++i) s[i] = mulmod(signed_res(noise[i], q), S->m, q); /* MForm :184 */
+    for (int i = 0; i + sl < d; ++i) sh[i + sl] = s[i];                          /* :186-190 */
+    for (int i = d - sl; i < d; ++i) sh[i - (d - sl)] = q - s[i];                  /* :191-195 */
+    uint64_t b = P->base % q;
+    for (int i = 0; i < d; ++i) { /* MulScalarThenSub :196 ; MForm(digits)+Add :198-199 */
+      uint64_t x = sh[i] % q, y = mulmod(s[i], b, q);
+      x = x >= y ? x - y : x + q - y;
+      uint64_t dm = mulmod(digits[i] % q, S->m, q);
+      x += dm;
+      if (x >= q) x -= q;
+      out[(size_t)l * d + i] = x;
+    }
+    r_ntt(S, out + (size_t)l * d); /* :200 */
+  }
+  free(digits);
+  free(s);
+  free(sh);
+}
+/* multi-word signed helpers for CRT rounding (rns.go:76-114) ------------------------------- */
+#define W 4 /* words: Q <= 4*61 bits */
+static void mw_from_u64(uint64_t* a, uint64_t v) { memset(a, 0, 8 * W); a[0] = v; }
+static void mw_muladd(uint64_t* a, uint64_t m, uint64_t add) { /* a = a*m + add */
+  uint64_t c = add;
+  for (int i = 0; i < W; ++i) {
+    u128 s = (u128)a[i] * m + c;
+    a[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+}
+static int mw_geq(const uint64_t* a, const uint64_t* b) { return geq(a, b, W); }
+/* centred CRT + arithmetic shift + per-prime Euclidean mod; residues r[nsrc] (plain, coeff
+ * domain) -> out[l] = (centre(V) >> cut) mod qo[l]. */
+static void crt_round(const of_subring* src, int nsrc, const uint64_t* r, int cut, const of_subring* dst, int ndst,
+                      uint64_t* out) {
+  int neg = 0;
+  uint64_t mag[W]; /* |value| before shift */
+  {
+    /* balanced fast path (rns.go:78-91); always taken for a single-prime ring */
+    int64_t b0 = (int64_t)(r[0] > (src[0].q >> 1) ? r[0] - src[0].q : r[0]);
+    int same = 1;
+    for (int j = 1; j < nsrc; ++j) {
+      int64_t bj = (int64_t)(r[j] > (src[j].q >> 1) ? r[j] - src[j].q : r[j]);
+      if (bj != b0) { same = 0; break; }
+    }
+    if (same) {
+      neg = b0 < 0;
+      mw_from_u64(mag, neg ? (uint64_t)(-(b0 + 1)) + 1 : (uint64_t)b0);
+      goto shifted;
+    }
+  }
+  {
+    /* Garner: V = x0 + q0*(x1 + q1*(x2 + ...)) in [0, Q)  (== sum r_j*gad_j mod Q, :93-99) */
+    uint64_t x[4];
+    for (int j = 0; j < nsrc; ++j) {
+      uint64_t q = src[j].q, v = r[j] % q;
+      for (int k = 0; k < j; ++k) { /* v = (v - x_k) * inv(q_k) mod q */
+        uint64_t xk = x[k] % q;
+        v = v >= xk ? v - xk : v + q - xk;
+        v = mulmod(v, powmod(src[k].q % q, q - 2, q), q);
+      }
+      x[j] = v;
+    }
+    uint64_t V[W], Q[W], Qh[W];
+    mw_from_u64(V, x[nsrc - 1]);
+    for (int j = nsrc - 2; j >= 0; --j) mw_muladd(V, src[j].q, x[j]);
+    mw_from_u64(Q, 1);
+    for (int j = 0; j < nsrc; ++j) mw_muladd(Q, src[j].q, 0);
+    shr_n(Qh, Q, W, 1);
+    if (mw_geq(V, Qh)) { /* acc >= Q>>1 -> acc - Q (:100-102) */
+      neg = 1;
+      sub_n(mag, Q, V, W);
+    } else {
+      memcpy(mag, V, 8 * W);
+    }
+  }
+shifted:;
+  /* floor shift (big.Int.Rsh): negative -> -ceil(mag / 2^cut) */
+  uint64_t sh[W];
+  memcpy(sh, mag, 8 * W);
+  int lost = 0;
+  for (int c = cut; c > 0;) {
+    int s = c > 63 ? 63 : c;
+    uint64_t lowmask = (1ull << s) - 1;
+    lost |= (sh[0] & lowmask) != 0;
+    shr_n(sh, sh, W, s);
+    c -= s;
+  }
+  if (neg && lost) { /* sh += 1 */
+    for (int k = 0; k < W; ++k) if (++sh[k]) break;
+  }
+  int zero = 1;
+  for (int k = 0; k < W; ++k) zero &= sh[k] == 0;
+  for (int l = 0; l < ndst; ++l) { /* setBigCoeffTo: Euclidean mod (rns.go:108-114) */
+    uint64_t q = dst[l].q;
+    u128 rr = 0;
+    for (int k = W - 1; k >= 0; --k) rr = ((rr << 64) | sh[k]) % q;
+    uint64_t m = (uint64_t)rr;
+    out[l] = (neg && !zero && m) ? q - m : m;
+  }
+}
+
+/* IMForm -> INTT -> CRT round -> MForm -> NTT in the destination ring (prover.go:164-176). */
+static void round_poly(const of_jindo* J, const of_subring* src, int nsrc, uint64_t* poly /* [nsrc][d] */, int cut,
+                       const of_subring* dst, int ndst, uint64_t* out /* [ndst][d] */) {
+  int d = J->P.d;
+  for (int l = 0; l < nsrc; ++l) {
+    uint64_t* p = poly + (size_t)l * d;
+    for (int k = 0; k < d; ++k) p[k] = mulmod(p[k], src[l].minv, src[l].q);
+    r_intt(&src[l], p);
+  }
+  uint64_t r[4], o[4];
+  for (int k = 0; k < d; ++k) {
+    for (int l = 0; l < nsrc; ++l) r[l] = poly[(size_t)l * d + k];
+    crt_round(src, nsrc, r, cut, dst, ndst, o);
+    for (int l = 0; l < ndst; ++l) out[(size_t)l * d + k] = mulmod(o[l], dst[l].m, dst[l].q);
+  }
+  for (int l = 0; l < ndst; ++l) r_ntt(&dst[l], out + (size_t)l * d);
+}
+
+static inline void mac_mont(uint64_t* acc, const uint64_t* a, const uint64_t* b, const of_subring* S, int d) {
+  for (int k = 0; k < d; ++k) { /* MulCoeffsMontgomeryThenAdd: acc += a*b*2^-64 */
+    uint64_t t = mulmod(mulmod(a[k], b[k], S->q), S->minv, S->q);
+    acc[k] += t;
+    if (acc[k] >= S->q) acc[k] -= S->q;
+  }
+}
+
+/* One commit.  See include/ringo.h rg_jindo_commit for every layout. */
+int of_jindo_commit(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
+                    const uint64_t* v, long nv, const uint64_t* last_row, const uint64_t* mask, const int64_t* enc_noise,
+                    const int64_t* mlwe_noise, uint64_t* o_incom, uint64_t* o_enc, uint64_t* o_mlwe, uint64_t* o_com) {
+  const of_jindo_params* P = &J->P;
+  int L = J->F.L, d = P->d, nq = P->nq, nqo = P->nqo, cs = P->cols * P->slots, nm = P->in_msis + P->mlwe;
+  if (nv > P->rank || nv < 1) return -1;
+  size_t polyq = (size_t)nq * d, polyo = (size_t)nqo * d;
+  uint64_t* first = (uint64_t*)calloc((size_t)cs * L, 8);
+  memcpy(first, v, 8 * L); /* genFirstLastRow (prover.go:74-83) */
+  uint64_t zero[MAXL] = {0};
+  for (int i = 1; i < cs; ++i)
+    f_sub(&J->F, first + (size_t)i * L, i < nv ? v + (size_t)i * L : zero, last_row + (size_t)(i - 1) * L, L);
+  memset(o_enc, 0, 8 * polyq * (size_t)(P->cols + 1) * P->rows);
+  uint64_t* com = (uint64_t*)malloc(8 * polyq);
+  for (int i = 0; i <= P->cols; ++i) {
+    const int64_t* en = enc_noise + (size_t)i * P->rows * d;
+    uint64_t* enc = o_enc + (size_t)i * P->rows * polyq;
+    int rs = i * P->slots, re = (i + 1) * P->slots;
+    if (i == P->cols) { /* prover.go:93-115 */
+      rand_encode(J, enc, mask, P->slots, en);
+      for (int j = 1; j < P->rows - 1; ++j) {
+        if ((long)j * cs > nv) break;
+        rand_encode(J, enc + (size_t)j * polyq, mask + (size_t)j * P->slots * L, P->slots, en + (size_t)j * d);
+      }
+      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, mask + (size_t)(P->rows - 1) * P->slots * L, P->slots,
+                  en + (size_t)(P->rows - 1) * d);
+    } else { /* prover.go:116-128 */
+      rand_encode(J, enc, first + (size_t)rs * L, P->slots, en);
+      for (int j = 1; j < P->rows - 1; ++j) {
+        long s0 = (long)j * cs + rs, e0 = (long)j * cs + re;
+        if (s0 > nv) break;
+        long e1 = e0 < nv ? e0 : nv;
+        rand_encode(J, enc + (size_t)j * polyq, v + (size_t)s0 * L, (int)(e1 - s0), en + (size_t)j * d);
+      }
+      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, last_row + (size_t)rs * L, P->slots,
+                  en + (size_t)(P->rows - 1) * d);
+    }
+    uint64_t* ml = o_mlwe + (size_t)i * nm * polyq; /* prover.go:130-142 */
+    for (int j = 0; j < nm; ++j) {
+      const int64_t* mn = mlwe_noise + ((size_t)i * nm + j) * d;
+      for (int l = 0; l < nq; ++l) {
+        const of_subring* S = &J->rq[l];
+        uint64_t* p = ml + (size_t)j * polyq + (size_t)l * d;
+        for (int k = 0; k < d; ++k) p[k] = mulmod(signed_res(mn[k], S->q), S->m, S->q);
+        r_ntt(S, p);
+      }
+    }
+    for (int j = 0; j < P->in_msis; ++j) { /* prover.go:149-176 */
+      for (int l = 0; l < nq; ++l) {
+        const of_subring* S = &J->rq[l];
+        uint64_t* acc = com + (size_t)l * d;
+        memset(acc, 0, 8 * (size_t)d);
+        for (int k = 0; k < P->rows; ++k)
+          mac_mont(acc, ck_in + (((size_t)j * P->rows + k) * nq + l) * d, enc + (size_t)k * polyq + (size_t)l * d, S, d);
+        for (int k = 0; k < P->mlwe; ++k)
+          mac_mont(acc, ck_mlwe + (((size_t)j * P->mlwe + k) * nq + l) * d, ml + (size_t)k * polyq + (size_t)l * d, S, d);
+        const uint64_t* e = ml + (size_t)(P->mlwe + j) * polyq + (size_t)l * d;
+        for (int k = 0; k < d; ++k) {
+          acc[k] += e[k];
+          if (acc[k] >= S->q) acc[k] -= S->q;
+        }
+      }
+      round_poly(J, J->rq, nq, com, P->log_in_cut, J->ro, nqo, o_incom + (size_t)(i * P->in_msis + j) * polyo);
+    }
+  }
+  /* outerCommitTo (prover.go:180-202) */
+  memset(o_com, 0, 8 * polyq * (size_t)P->out_msis);
+  uint64_t* oc = (uint64_t*)malloc(8 * polyo);
+  for (int i = 0; i < P->out_msis; ++i) {
+    for (int l = 0; l < nqo; ++l) {
+      uint64_t* acc = oc + (size_t)l * d;
+      memset(acc, 0, 8 * (size_t)d);
+      for (int j = 0; j < P->dcmp; ++j)
+        mac_mont(acc, ck_out + (((size_t)i * P->dcmp + j) * nqo + l) * d, o_incom + (size_t)j * polyo + (size_t)l * d,
+                 &J->ro[l], d);
+    }
+    round_poly(J, J->ro, nqo, oc, P->log_out_cut, J->ro, nqo, o_com + (size_t)i * polyq);
+  }
+  free(oc);
+  free(com);
+  free(first);
+  return 0;
+}
