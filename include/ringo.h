@@ -1,0 +1,189 @@
+/* ringo.h -- C ABI of libringo, the MI355X (gfx950) implementation of ringo-snark's
+ * NTT / Jindo-commit hot path.
+ *
+ * Every entry point is what the reference's Go side would bind through cgo (see
+ * INTEGRATION.md for the binding).  The reference interface each one replaces is cited as
+ * path:line into sp301415/ringo-snark.  Plain pointers and sizes only; no torch types.
+ *
+ * Conventions
+ *  - Field elements are gnark `Uint [L]uint64` values in Montgomery form (R = 2^(64L)),
+ *    little-endian limbs, fully reduced (jindo/internal/zp/element.go:37-51).  A polynomial
+ *    of rank N is N consecutive elements: layout [N][L] (what a contiguous []zp.Uint holds).
+ *  - Batched calls take [batch][N][L] with polys back to back.
+ *  - Jindo ring polynomials use Lattigo's limb-major layout Coeffs[limb][coeff]
+ *    (ring.Poly, lattigo/v6 v6.1.0).
+ *  - `*_dev` entry points take DEVICE pointers and a hipStream_t (passed as void*; NULL =
+ *    the null stream) and are asynchronous.  Entry points without `_dev` take HOST pointers
+ *    and are synchronous (they stage through library-owned device buffers).
+ *  - Outputs may alias inputs exactly (out == in); partial overlap is invalid.
+ *  - Return value: RG_OK or a negative rg_status; the library never aborts.  The Go shim
+ *    maps the codes to the reference's panics (messages in rg_status_string).
+ *  - Handles are immutable after creation and may be shared by threads; each call is
+ *    thread-safe (host staging is per call).
+ */
+#ifndef RINGO_H
+#define RINGO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  RG_OK = 0,
+  RG_ERR_INVALID = -1,     /* shape/argument error  -> Go panic "inconsistent input(s)" */
+  RG_ERR_NOT_POW2 = -2,    /* ntt.go:27-29,154-156  "rank must be a power of two" */
+  RG_ERR_UNSUPPORTED = -3, /* ntt.go:35-37,162-164  "NTT not supported" */
+  RG_ERR_DEVICE = -4,      /* HIP runtime error (message via rg_last_error) */
+  RG_ERR_NOMEM = -5,
+  RG_ERR_RANK = -6         /* jindo/prover.go:46-49 "len(v) > params.rank" */
+} rg_status;
+
+const char* rg_status_string(int status);
+/* Thread-local text of the last device error (hipGetErrorString + call site). */
+const char* rg_last_error(void);
+/* Library build id (kernel set + gfx target), for logs. */
+const char* rg_version(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* Field (math/bignum.Uint[E], gnark-generated zp.Uint)                                   */
+/* ------------------------------------------------------------------------------------ */
+typedef struct rg_field rg_field;
+
+/* Replaces the compile-time field type E.  q_le: the modulus as `limbs` little-endian
+ * words (zp.q0..q{L-1}, element.go:47-50).  The library derives qInvNeg (element.go:72) and
+ * R^2 (element.go:784) itself; rg_field_constants exposes them for cross-checks.
+ * limbs in 1..16. */
+rg_status rg_field_create(int limbs, const uint64_t* q_le, rg_field** out);
+void rg_field_destroy(rg_field* f);
+int rg_field_limbs(const rg_field* f);
+/* qinv_neg: -q^-1 mod 2^64; r2_le, one_le: R^2 mod q and R mod q (limbs words each). */
+rg_status rg_field_constants(const rg_field* f, uint64_t* qinv_neg, uint64_t* r2_le, uint64_t* one_le);
+
+/* ------------------------------------------------------------------------------------ */
+/* bigpoly transformers (math/bigpoly/ntt.go)                                             */
+/* ------------------------------------------------------------------------------------ */
+typedef struct rg_ntt rg_ntt;
+
+/* Replaces NewCyclotomicTransformer (negacyclic=1, ntt.go:153-203) and
+ * NewCyclicTransformer (negacyclic=0, ntt.go:26-95).  The library derives psi/omega by the
+ * reference's generator search (first x = 2,3,... ; ntt.go:46-53,173-180) and builds the
+ * twiddle tables itself. */
+rg_status rg_ntt_create(const rg_field* f, int rank, int negacyclic, rg_ntt** out);
+/* Same, but with the tables taken verbatim from the Go transformer (tw, twInv: rank
+ * elements each in Montgomery form, laid out [rank][L]; rank_inv: one element), so twiddle
+ * parity holds by construction.  Tables are validated (tw[0] == twInv[0] == 1). */
+rg_status rg_ntt_create_from_tables(const rg_field* f, int rank, int negacyclic, const uint64_t* tw,
+                                    const uint64_t* tw_inv, const uint64_t* rank_inv, rg_ntt** out);
+void rg_ntt_destroy(rg_ntt* t);
+int rg_ntt_rank(const rg_ntt* t); /* Rank() (ntt.go:139,469) */
+/* Copy the tables out (Montgomery, [rank][L] each + one element). */
+rg_status rg_ntt_tables(const rg_ntt* t, uint64_t* tw, uint64_t* tw_inv, uint64_t* rank_inv);
+
+/* FwdNTTTo(vOut, v) (ntt.go:98-115,206-223) on `batch` polys: natural -> bit-reversed. */
+rg_status rg_ntt_fwd(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t batch);
+rg_status rg_ntt_fwd_dev(const rg_ntt* t, uint64_t* d_out, const uint64_t* d_in, size_t batch, void* stream);
+/* InvNTTTo(vOut, v) (ntt.go:118-136,226-244): bit-reversed -> natural, times rank^-1. */
+rg_status rg_ntt_inv(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t batch);
+rg_status rg_ntt_inv_dev(const rg_ntt* t, uint64_t* d_out, const uint64_t* d_in, size_t batch, void* stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Pointwise ops (math/bigpoly/vec.go:9-121 via baseOperator, base_op.go:49-171)         */
+/* ------------------------------------------------------------------------------------ */
+typedef enum {
+  RG_VEC_ADD = 0,      /* out = a + b        AddTo        base_op.go:49-55   */
+  RG_VEC_SUB = 1,      /* out = a - b        SubTo        base_op.go:64-70   */
+  RG_VEC_NEG = 2,      /* out = -a           NegTo        base_op.go:79-85   */
+  RG_VEC_MUL = 3,      /* out = a * b        MulTo        base_op.go:133-142 */
+  RG_VEC_SMUL = 4,     /* out = a * c        ScalarMulTo  base_op.go:94-100 */
+  RG_VEC_MUL_ADD = 5,  /* out += a * b       MulAddTo     base_op.go:144-157 */
+  RG_VEC_MUL_SUB = 6,  /* out -= a * b       MulSubTo     base_op.go:159-172 */
+  RG_VEC_SMUL_ADD = 7, /* out += a * c       ScalarMulAddTo base_op.go:102-112 */
+  RG_VEC_SMUL_SUB = 8  /* out -= a * c       ScalarMulSubTo base_op.go:114-124 */
+} rg_vec_op;
+
+/* n elements ([n][L]).  For the SMUL* ops `b` points to ONE element (the scalar c);
+ * for NEG `b` is ignored.  Domain checks (IsNTT flags) stay in the caller, as in Go. */
+rg_status rg_vec(const rg_field* f, int op, uint64_t* out, const uint64_t* a, const uint64_t* b, size_t n);
+rg_status rg_vec_dev(const rg_field* f, int op, uint64_t* d_out, const uint64_t* d_a, const uint64_t* d_b, size_t n,
+                     void* stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Jindo commitment (jindo/params.go, encoder.go, rns.go, prover.go, entities.go)         */
+/* ------------------------------------------------------------------------------------ */
+/* Shapes exactly as jindo.Parameters holds them (params.go:64-123); taken from Go
+ * (NewParameters' float search is not re-derived here). */
+typedef struct {
+  int rank, rows, cols, slots; /* Rank() Rows() Cols() Slots()                      */
+  int exp;                     /* Exp(): digits per element (k)                      */
+  int d;                       /* ring degree = max(k, 256)                          */
+  int in_msis, out_msis, mlwe; /* InMSISRank() OutMSISRank() MLWERank()              */
+  int dcmp;                    /* InCommitDecomposeLen()                             */
+  int log_in_cut, log_out_cut; /* LogInCutOff() OutCutOff()                          */
+  uint64_t base;               /* Base(): b with p = b^k + 1                          */
+  int nq, nqo;                 /* limbs of RingQ() / RingQOut() (1..4, nqo <= nq)    */
+  uint64_t q[4], qo[4];        /* RingQ().ModuliChain(), RingQOut().ModuliChain()   */
+  int field_limbs;             /* L of E                                             */
+  uint64_t field_q[16];        /* modulus of E, little-endian                        */
+} rg_jindo_params;
+
+typedef struct rg_jindo rg_jindo;
+
+/* NewProver's deterministic part (prover.go:28-40): builds RNS NTT tables (Lattigo
+ * convention: smallest primitive root >= 3) and uploads the commit key.
+ * ck_in   [in_msis][rows][nq][d]   CommitKey.In   (entities.go:24-35)
+ * ck_mlwe [in_msis][mlwe][nq][d]   CommitKey.MLWE (entities.go:37-48)
+ * ck_out  [out_msis][dcmp][nqo][d] CommitKey.Out  (entities.go:50-61)                 */
+rg_status rg_jindo_create(const rg_jindo_params* p, const uint64_t* ck_in, const uint64_t* ck_mlwe,
+                          const uint64_t* ck_out, rg_jindo** out);
+/* Same, deriving the commit key from the CRS exactly as NewCommitKey does
+ * (SHA-384 -> AES-256-CTR -> SampleN, entities.go:21-73, uniform.go:38-95). */
+rg_status rg_jindo_create_from_crs(const rg_jindo_params* p, const uint8_t* crs, size_t crs_len, rg_jindo** out);
+void rg_jindo_destroy(rg_jindo* j);
+/* Copy the commit key out (same layouts as rg_jindo_create). */
+rg_status rg_jindo_commit_key(const rg_jindo* j, uint64_t* ck_in, uint64_t* ck_mlwe, uint64_t* ck_out);
+
+/* Prover.Commit (prover.go:45-62) with the randomness INJECTED so the result is
+ * bit-exact against Go given the same draws:
+ *  v          [nv][L]  the committed vector, Montgomery (1 <= nv <= rank)
+ *  last_row   [cols*slots][L]  genFirstLastRow's MustSetRandom draws, last entry 0 (:68-72)
+ *  mask       [rows][slots][L] the mask column's MustSetRandom draws, one row per
+ *                              randEncodeTo (:95-115; rows the reference skips are ignored)
+ *  enc_noise  [cols+1][rows][d] int64  the Gaussian samples c of each randEncodeTo
+ *                              (encoder.go:166-183, TwinCDT or COSAC)
+ *  mlwe_noise [cols+1][in_msis+mlwe][d] int64  the MLWE samples (prover.go:130-139)
+ * Outputs (Lattigo limb-major residues, NTT + Montgomery domain, as Go holds them):
+ *  o_incom  [dcmp][nqo][d]              Opening.InCommit
+ *  o_enc    [cols+1][rows][nq][d]       Opening.Encode   (skipped rows = 0, as in Go)
+ *  o_mlwe   [cols+1][in_msis+mlwe][nq][d]  Opening.MLWE
+ *  o_com    [out_msis][nq][d]           Commitment.Value (rows >= nqo are 0: the reference
+ *                                       allocates ringQ polys, entities.go:85-94)       */
+rg_status rg_jindo_commit(const rg_jindo* j, const uint64_t* v, size_t nv, const uint64_t* last_row,
+                          const uint64_t* mask, const int64_t* enc_noise, const int64_t* mlwe_noise,
+                          uint64_t* o_incom, uint64_t* o_enc, uint64_t* o_mlwe, uint64_t* o_com);
+/* Device-resident batch: `batch` independent commits of equal length nv; every array above
+ * gains a leading [batch] dimension.  Asynchronous on `stream`. */
+rg_status rg_jindo_commit_dev(const rg_jindo* j, size_t batch, const uint64_t* d_v, size_t nv,
+                              const uint64_t* d_last_row, const uint64_t* d_mask, const int64_t* d_enc_noise,
+                              const int64_t* d_mlwe_noise, uint64_t* d_incom, uint64_t* d_enc, uint64_t* d_mlwe,
+                              uint64_t* d_com, void* stream);
+/* Bytes of device scratch rg_jindo_commit_dev needs for `batch` commits (allocated and
+ * cached inside the handle on first use; exposed for capacity planning). */
+size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
+
+/* ------------------------------------------------------------------------------------ */
+/* Device memory helpers (so a cgo caller needs no HIP headers)                           */
+/* ------------------------------------------------------------------------------------ */
+rg_status rg_malloc(void** d_ptr, size_t bytes);
+rg_status rg_free(void* d_ptr);
+rg_status rg_memcpy_h2d(void* d_dst, const void* src, size_t bytes, void* stream);
+rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream);
+rg_status rg_stream_sync(void* stream);
+rg_status rg_set_device(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RINGO_H */

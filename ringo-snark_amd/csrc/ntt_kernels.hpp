@@ -1,0 +1,476 @@
+// ntt_kernels.hpp -- bigpoly negacyclic / cyclic NTT kernels for gfx950 (math/bigpoly/ntt.go).
+//
+// What is computed (bit-exact vs the reference):
+//   forward  = nttInPlace   (ntt.go:246-355): Cooley-Tukey DIT, natural in -> bit-reversed out,
+//              butterfly (u, v) <- (u + w v, u - w v) with w = tw[m + i]        (ntt.go:254-259)
+//   inverse  = inttInPlace + scalarMulVecTo(N^-1) (ntt.go:357-466, 242-243): Gentleman-Sande,
+//              (u, v) <- (u + v, (u - v) w), w = twInv[m + i]; the N^-1 scaling is fused into
+//              the last stage ((u+v) N^-1, (u-v)(twInv[1] N^-1)) -- same residues.
+// The table layout tw[m + i] is shared by the cyclic and negacyclic transformers, so one
+// kernel family serves both (only the tables differ).
+//
+// How (MI355X-first):
+//   A transform of N = 2^logN points is split into passes; a pass covers P consecutive
+//   global stages [G0, G0+P) and decomposes into independent 2^P-point sub-transforms whose
+//   points sit at stride S = 2^(logN-G0-P) (G0 = 0: "column" pass, S = 1: "row" pass).
+//   One 256-thread workgroup owns SW = 256 / 2^(P-R) sub-transforms:
+//     1. the tile is read from HBM with 16-B coalesced loads into LDS (limb planes, one pad
+//        slot per 16 points so every round's ds_read_b64/ds_write_b64 is conflict-free),
+//     2. ceil(P/R) rounds: each thread pulls 2^R points into VGPRs, runs R radix-2 stages
+//        in registers (twiddles from the L2-resident table), writes them back,
+//     3. the tile is written back with coalesced 16-B stores (in place is allowed).
+//   N = 2^16 at L = 1 is two passes of 8 stages (column then row; reversed for the inverse).
+//   The batch of polynomials is processed in MALL-sized chunks (column pass, row pass per
+//   chunk) so the pass-to-pass intermediate stays in the 256 MiB Infinity Cache and HBM
+//   sees ~one read and one write per element per transform.
+#pragma once
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+#include "field.hpp"
+#include "ntt_plan.hpp"
+
+namespace rg {
+
+constexpr int kWG = 256;
+
+template <int L>
+struct NttArgs {
+  const uint64_t* in;
+  uint64_t* out;
+  const uint64_t* tw;  // L==1 && SHOUP: (w, w') pairs [N][2]; else Montgomery [N][L]
+  FieldParams<L> F;
+  uint64_t nsc[L];   // N^-1: Montgomery form (or plain value for SHOUP)
+  uint64_t nsc_sh;   // Shoup companion of nsc
+  uint64_t w1n[L];   // twInv[1] * N^-1
+  uint64_t w1n_sh;
+  int logN, G0;
+  long long total_sub;  // batch * N / 2^P
+};
+
+// per-L register radix (points per thread = 2^R) keeps VGPR use near 128
+template <int L>
+struct RadixOf {
+  static constexpr int value = (L == 1 || L == 2) ? 4 : (L <= 4 ? 3 : (L <= 7 ? 2 : 2));
+};
+template <int L>
+constexpr int pmax_of() {
+  return RadixOf<L>::value + 8;
+}
+
+template <int L, bool SHOUP>
+struct Tw {
+  uint64_t w[L];
+  uint64_t wp;
+};
+
+template <int L, bool SHOUP>
+__device__ __forceinline__ void load_tw(Tw<L, SHOUP>& w, const uint64_t* tw, long long idx) {
+  if constexpr (SHOUP) {
+    const ulonglong2 v = reinterpret_cast<const ulonglong2*>(tw)[idx];
+    w.w[0] = v.x;
+    w.wp = v.y;
+  } else {
+#pragma unroll
+    for (int l = 0; l < L; ++l) w.w[l] = tw[idx * L + l];
+  }
+}
+
+template <int L, bool SHOUP>
+__device__ __forceinline__ void mul_tw(uint64_t* z, const uint64_t* x, const Tw<L, SHOUP>& w,
+                                       const FieldParams<L>& F) {
+  if constexpr (SHOUP) {
+    z[0] = shoup_mul(x[0], w.w[0], w.wp, F.q[0]);
+  } else {
+    f_mul<L>(z, x, w.w, F);
+  }
+}
+
+// forward CT butterfly (ntt.go:254-259)
+template <int L, bool SHOUP>
+__device__ __forceinline__ void bfly_fwd(uint64_t* u, uint64_t* v, const Tw<L, SHOUP>& w, const FieldParams<L>& F) {
+  uint64_t t[L];
+  mul_tw<L, SHOUP>(t, v, w, F);
+  if constexpr (L == 1 && SHOUP) {  // q < 2^63: 2q fits a word
+    uint64_t a = u[0];
+    u[0] = mod_add(a, t[0], F.q[0]);
+    v[0] = mod_sub(a, t[0], F.q[0]);
+  } else {
+    f_sub<L>(v, u, t, F);
+    f_add<L>(u, u, t, F);
+  }
+}
+// inverse GS butterfly (ntt.go:365-370)
+template <int L, bool SHOUP>
+__device__ __forceinline__ void bfly_inv(uint64_t* u, uint64_t* v, const Tw<L, SHOUP>& w, const FieldParams<L>& F) {
+  uint64_t d[L];
+  if constexpr (L == 1 && SHOUP) {
+    uint64_t a = u[0], b = v[0];
+    u[0] = mod_add(a, b, F.q[0]);
+    d[0] = mod_sub(a, b, F.q[0]);
+  } else {
+    f_sub<L>(d, u, v, F);
+    f_add<L>(u, u, v, F);
+  }
+  mul_tw<L, SHOUP>(v, d, w, F);
+}
+
+__device__ __forceinline__ int padx(int x) { return x + (x >> 4); }
+
+// ----------------------------------------------------------------------------------------
+// rounds
+// ----------------------------------------------------------------------------------------
+template <int L, int P, int R, bool INV, bool SHOUP, bool SCALE, int K>
+__device__ __forceinline__ void do_rounds(const NttArgs<L>& a, uint64_t* lds, int s, int t, long long hi,
+                                          int plane) {
+  constexpr int NR = (P + R - 1) / R;
+  constexpr int R0 = P - R * (NR - 1);
+  constexpr int RK = (K == 0) ? R0 : R;
+  constexpr int NG = 1 << (R - RK);  // groups per thread this round
+  constexpr int NPK = 1 << RK;
+  // bit window of this round
+  constexpr int LO = INV ? ((K == 0) ? 0 : R0 + R * (K - 1)) : (P - ((K == 0) ? 0 : R0 + R * (K - 1)) - RK);
+  constexpr int HI = LO + RK;
+  const int PADN = (1 << P) + ((1 << P) >> 4);
+  uint64_t* ls = lds + (long long)s * PADN;
+
+#pragma unroll 1
+  for (int g = 0; g < NG; ++g) {
+    const int o = t * NG + g;                   // index over the bits outside [LO, HI)
+    const int o_low = o & ((1 << LO) - 1);
+    const int o_high = o >> LO;                 // bits above HI
+    const int xbase = (o_high << HI) | o_low;
+    uint64_t e[NPK][L];
+#pragma unroll
+    for (int y = 0; y < NPK; ++y) {
+      const int x = xbase | (y << LO);
+#pragma unroll
+      for (int l = 0; l < L; ++l) e[y][l] = ls[(long long)l * plane + padx(x)];
+    }
+    if constexpr (!INV) {
+#pragma unroll
+      for (int sp = 0; sp < RK; ++sp) {
+        const int gp = P - HI + sp;  // local stage index (0 = first stage of the pass)
+        const int half = NPK >> (sp + 1);
+#pragma unroll
+        for (int blk = 0; blk < (1 << sp); ++blk) {
+          const long long idx = (1LL << (a.G0 + gp)) + (hi << gp) + ((long long)o_high << sp) + blk;
+          Tw<L, SHOUP> w;
+          load_tw<L, SHOUP>(w, a.tw, idx);
+#pragma unroll
+          for (int u = 0; u < half; ++u) {
+            const int i0 = blk * 2 * half + u;
+            bfly_fwd<L, SHOUP>(e[i0], e[i0 + half], w, a.F);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int sp = 0; sp < RK; ++sp) {
+        const int gp = P - 1 - (LO + sp);
+        const int half = 1 << sp;
+        const bool last = SCALE && (a.G0 + gp == 0);
+#pragma unroll
+        for (int blk = 0; blk < (NPK >> (sp + 1)); ++blk) {
+          const long long idx =
+              (1LL << (a.G0 + gp)) + (hi << gp) + ((long long)o_high << (RK - sp - 1)) + blk;
+          Tw<L, SHOUP> w;
+          if (last) {
+#pragma unroll
+            for (int l = 0; l < L; ++l) w.w[l] = a.w1n[l];
+            w.wp = a.w1n_sh;
+          } else {
+            load_tw<L, SHOUP>(w, a.tw, idx);
+          }
+#pragma unroll
+          for (int u = 0; u < half; ++u) {
+            const int i0 = blk * 2 * half + u;
+            bfly_inv<L, SHOUP>(e[i0], e[i0 + half], w, a.F);
+            if (last) {  // (u + v) * N^-1
+              Tw<L, SHOUP> ns;
+#pragma unroll
+              for (int l = 0; l < L; ++l) ns.w[l] = a.nsc[l];
+              ns.wp = a.nsc_sh;
+              uint64_t z[L];
+              mul_tw<L, SHOUP>(z, e[i0], ns, a.F);
+#pragma unroll
+              for (int l = 0; l < L; ++l) e[i0][l] = z[l];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int y = 0; y < NPK; ++y) {
+      const int x = xbase | (y << LO);
+#pragma unroll
+      for (int l = 0; l < L; ++l) ls[(long long)l * plane + padx(x)] = e[y][l];
+    }
+  }
+  __syncthreads();
+  if constexpr (K + 1 < NR) do_rounds<L, P, R, INV, SHOUP, SCALE, K + 1>(a, lds, s, t, hi, plane);
+}
+
+// ----------------------------------------------------------------------------------------
+// pass kernel
+// ----------------------------------------------------------------------------------------
+template <int L, int P, bool INV, bool SHOUP, bool SCALE>
+__global__ __launch_bounds__(kWG) void ntt_pass_kernel(NttArgs<L> a) {
+  constexpr int R = (RadixOf<L>::value < P) ? RadixOf<L>::value : P;
+  constexpr int NP = 1 << P;
+  constexpr int TS = 1 << (P - R);
+  constexpr int SW = kWG / TS;
+  constexpr int PADN = NP + (NP >> 4);
+  constexpr int PLANE = SW * PADN;  // u64 per limb plane
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+
+  const int logN = a.logN;
+  const int logS = logN - a.G0 - P;
+  const long long S = 1LL << logS;
+  const int nlo = (int)(S < SW ? S : SW);
+  const int nhi = SW / nlo;
+  const long long sub0 = (long long)blockIdx.x * SW;
+  const long long rowid0 = sub0 >> logS;
+  const long long lo0 = sub0 & (S - 1);
+  const int rowshift = logN - a.G0;  // log2 of the row pitch in elements
+  const long long total = a.total_sub;
+
+  // ---- 1. HBM -> LDS (coalesced) ----
+  // flat element e = (sr * NP + x) * nlo + sl
+  constexpr int NE = SW * NP;
+  const bool pairs = (L % 2 == 0) || (nlo % 2 == 0) || (nlo == (int)S);
+  if (pairs) {
+    const int NU = NE * L / 2;  // u64 pairs in the tile
+    for (int f2 = threadIdx.x; f2 < NU; f2 += kWG) {
+      const int f = 2 * f2;
+      const int e = f / L, l = f % L;
+      const int sl = e % nlo, xr = e / nlo, x = xr % NP, sr = xr / NP;
+      const int s = sr * nlo + sl;
+      if (sub0 + s >= total) continue;
+      const long long addr = (((rowid0 + sr) << rowshift) + (long long)x * S + lo0 + sl) * L + l;
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(a.in + addr);
+      lds[(long long)l * PLANE + s * PADN + padx(x)] = v.x;
+      // second word: next limb of the same element, or limb 0 of the next element
+      const int f1 = f + 1;
+      const int e1 = f1 / L, l1 = f1 % L;
+      const int sl1 = e1 % nlo, xr1 = e1 / nlo, x1 = xr1 % NP, sr1 = xr1 / NP;
+      const int s1 = sr1 * nlo + sl1;
+      lds[(long long)l1 * PLANE + s1 * PADN + padx(x1)] = v.y;
+    }
+  } else {
+    const int NU = NE * L;
+    for (int f = threadIdx.x; f < NU; f += kWG) {
+      const int e = f / L, l = f % L;
+      const int sl = e % nlo, xr = e / nlo, x = xr % NP, sr = xr / NP;
+      const int s = sr * nlo + sl;
+      if (sub0 + s >= total) continue;
+      const long long addr = (((rowid0 + sr) << rowshift) + (long long)x * S + lo0 + sl) * L + l;
+      lds[(long long)l * PLANE + s * PADN + padx(x)] = a.in[addr];
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. rounds ----
+  const int s = threadIdx.x / TS;
+  const int t = threadIdx.x % TS;
+  const long long rowid = rowid0 + s / nlo;
+  const long long hi = rowid & ((1LL << a.G0) - 1);  // row index within the polynomial
+  do_rounds<L, P, R, INV, SHOUP, SCALE, 0>(a, lds, s, t, hi, PLANE);
+
+  // ---- 3. LDS -> HBM ----
+  if (pairs) {
+    const int NU = NE * L / 2;
+    for (int f2 = threadIdx.x; f2 < NU; f2 += kWG) {
+      const int f = 2 * f2;
+      const int e = f / L, l = f % L;
+      const int sl = e % nlo, xr = e / nlo, x = xr % NP, sr = xr / NP;
+      const int s0 = sr * nlo + sl;
+      if (sub0 + s0 >= total) continue;
+      const long long addr = (((rowid0 + sr) << rowshift) + (long long)x * S + lo0 + sl) * L + l;
+      const int f1 = f + 1;
+      const int e1 = f1 / L, l1 = f1 % L;
+      const int sl1 = e1 % nlo, xr1 = e1 / nlo, x1 = xr1 % NP, sr1 = xr1 / NP;
+      const int s1 = sr1 * nlo + sl1;
+      ulonglong2 v;
+      v.x = lds[(long long)l * PLANE + s0 * PADN + padx(x)];
+      v.y = lds[(long long)l1 * PLANE + s1 * PADN + padx(x1)];
+      *reinterpret_cast<ulonglong2*>(a.out + addr) = v;
+    }
+  } else {
+    const int NU = NE * L;
+    for (int f = threadIdx.x; f < NU; f += kWG) {
+      const int e = f / L, l = f % L;
+      const int sl = e % nlo, xr = e / nlo, x = xr % NP, sr = xr / NP;
+      const int s0 = sr * nlo + sl;
+      if (sub0 + s0 >= total) continue;
+      const long long addr = (((rowid0 + sr) << rowshift) + (long long)x * S + lo0 + sl) * L + l;
+      a.out[addr] = lds[(long long)l * PLANE + s0 * PADN + padx(x)];
+    }
+  }
+}
+
+template <int L, int P>
+constexpr size_t lds_bytes() {
+  constexpr int R = (RadixOf<L>::value < P) ? RadixOf<L>::value : P;
+  constexpr int NP = 1 << P;
+  constexpr int SW = kWG / (1 << (P - R));
+  return (size_t)SW * (NP + (NP >> 4)) * L * 8;
+}
+
+
+// ----------------------------------------------------------------------------------------
+// compact per-stage kernel: one thread per butterfly, one launch per stage.  Used for small
+// ranks (logN < kMinTiledP) and for the wide buckler fields (L = 7, 14) where a register-
+// tiled pass would be dominated by code size rather than bandwidth.
+// ----------------------------------------------------------------------------------------
+template <int L, bool INV, bool SHOUP>
+__global__ __launch_bounds__(256) void ntt_stage_kernel(NttArgs<L> a, int lt, int scale) {
+  const long long half_n = 1LL << (a.logN - 1);
+  const long long total = a.total_sub * half_n;  // total_sub = batch here
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += stride) {
+    const long long b = k >> (a.logN - 1);
+    const long long r = k & (half_n - 1);
+    const long long t = 1LL << lt;
+    const long long m = 1LL << (a.logN - 1 - lt);
+    const long long i = r >> lt;
+    const long long j = (i << (lt + 1)) + (r & (t - 1));
+    const uint64_t* src = a.in + (b << a.logN) * L;
+    uint64_t* dst = a.out + (b << a.logN) * L;
+    uint64_t u[L], v[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      u[l] = src[j * L + l];
+      v[l] = src[(j + t) * L + l];
+    }
+    Tw<L, SHOUP> w;
+    if (INV && scale) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) w.w[l] = a.w1n[l];
+      w.wp = a.w1n_sh;
+    } else {
+      load_tw<L, SHOUP>(w, a.tw, m + i);
+    }
+    if constexpr (!INV) {
+      bfly_fwd<L, SHOUP>(u, v, w, a.F);
+    } else {
+      bfly_inv<L, SHOUP>(u, v, w, a.F);
+      if (scale) {
+        Tw<L, SHOUP> ns;
+#pragma unroll
+        for (int l = 0; l < L; ++l) ns.w[l] = a.nsc[l];
+        ns.wp = a.nsc_sh;
+        uint64_t z[L];
+        mul_tw<L, SHOUP>(z, u, ns, a.F);
+#pragma unroll
+        for (int l = 0; l < L; ++l) u[l] = z[l];
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      dst[j * L + l] = u[l];
+      dst[(j + t) * L + l] = v[l];
+    }
+  }
+}
+
+// smallest P handled by the LDS-tiled pass kernel (smaller transforms use stage kernels)
+constexpr int kMinTiledP = 6;
+
+template <int L>
+static void fill_args(NttArgs<L>& a, const NttLaunch& p) {
+  memcpy(a.F.q, p.q, 8 * L);
+  a.F.qinv = p.qinv;
+  memcpy(a.nsc, p.nsc, 8 * L);
+  a.nsc_sh = p.nsc_sh;
+  memcpy(a.w1n, p.w1n, 8 * L);
+  a.w1n_sh = p.w1n_sh;
+  a.logN = p.logN;
+  a.tw = p.tw;
+}
+
+template <int L, int P, bool INV, bool SHOUP, bool SCALE>
+static rg_status launch_pass(const NttArgs<L>& a, hipStream_t st) {
+  constexpr int R = (RadixOf<L>::value < P) ? RadixOf<L>::value : P;
+  constexpr int SW = kWG / (1 << (P - R));
+  const long long grid = (a.total_sub + SW - 1) / SW;
+  constexpr size_t lds = lds_bytes<L, P>();
+  static_assert(lds <= 160 * 1024, "tile exceeds LDS");
+  auto k = ntt_pass_kernel<L, P, INV, SHOUP, SCALE>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, st, a);
+  return check_launch("ntt_pass");
+}
+
+template <int L, bool INV, bool SHOUP, bool SCALE, int P = kMinTiledP>
+static rg_status dispatch_P(int p, const NttArgs<L>& a, hipStream_t st) {
+  if constexpr (P > pmax_of<L>()) {
+    return RG_ERR_UNSUPPORTED;
+  } else {
+    if (p == P) return launch_pass<L, P, INV, SHOUP, SCALE>(a, st);
+    return dispatch_P<L, INV, SHOUP, SCALE, P + 1>(p, a, st);
+  }
+}
+
+template <int L, bool SHOUP>
+static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
+  const size_t N = (size_t)1 << p.logN;
+  const size_t poly_u64 = N * L;
+  // chunk the batch so the pass-to-pass intermediate stays in the 256 MiB Infinity Cache
+  size_t chunk = std::max<size_t>(1, (size_t)(96ull << 20) / (poly_u64 * 8));
+  if (p.npasses == 1) chunk = p.batch;
+  NttArgs<L> a;
+  fill_args<L>(a, p);
+  for (size_t b0 = 0; b0 < p.batch; b0 += chunk) {
+    const size_t nb = std::min(chunk, p.batch - b0);
+    for (int k = 0; k < p.npasses; ++k) {
+      const PassDesc& ps = p.inv ? p.passes[p.npasses - 1 - k] : p.passes[k];
+      a.in = (k == 0 ? p.in : p.out) + b0 * poly_u64;
+      a.out = p.out + b0 * poly_u64;
+      a.G0 = ps.G0;
+      a.total_sub = (long long)nb * (long long)(N >> ps.P);
+      rg_status s;
+      if (!p.inv)
+        s = dispatch_P<L, false, SHOUP, false>(ps.P, a, st);
+      else if (ps.G0 == 0)
+        s = dispatch_P<L, true, SHOUP, true>(ps.P, a, st);
+      else
+        s = dispatch_P<L, true, SHOUP, false>(ps.P, a, st);
+      RG_TRY(s);
+    }
+  }
+  return RG_OK;
+}
+
+template <int L, bool SHOUP>
+static rg_status run_stages(const NttLaunch& p, hipStream_t st) {
+  NttArgs<L> a;
+  fill_args<L>(a, p);
+  a.G0 = 0;
+  a.total_sub = (long long)p.batch;
+  const long long nbfly = (long long)p.batch << (p.logN - 1);
+  long long blocks = (nbfly + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  for (int s = 0; s < p.logN; ++s) {
+    // forward: t = N/2 .. 1 (lt = logN-1 .. 0); inverse: t = 1 .. N/2
+    const int lt = p.inv ? s : p.logN - 1 - s;
+    a.in = (s == 0) ? p.in : p.out;
+    a.out = p.out;
+    const int scale = (p.inv && lt == p.logN - 1) ? 1 : 0;
+    if (p.inv)
+      hipLaunchKernelGGL((ntt_stage_kernel<L, true, SHOUP>), dim3((unsigned)blocks), dim3(256), 0, st, a, lt, scale);
+    else
+      hipLaunchKernelGGL((ntt_stage_kernel<L, false, SHOUP>), dim3((unsigned)blocks), dim3(256), 0, st, a, lt, scale);
+    RG_TRY(check_launch("ntt_stage"));
+  }
+  return RG_OK;
+}
+
+}  // namespace rg

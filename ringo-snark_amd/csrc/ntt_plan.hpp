@@ -1,0 +1,35 @@
+// ntt_plan.hpp -- what ntt.hip hands to the per-limb-count kernel translation units.
+#pragma once
+#include "common.hpp"
+
+namespace rg {
+
+struct PassDesc {
+  int G0, P;
+};
+
+// Everything a per-L translation unit needs from the host plan.
+struct NttLaunch {
+  const uint64_t* in;
+  uint64_t* out;
+  const uint64_t* tw;
+  const uint64_t* q;
+  uint64_t qinv;
+  const uint64_t* nsc;
+  uint64_t nsc_sh;
+  const uint64_t* w1n;
+  uint64_t w1n_sh;
+  int logN;
+  bool shoup, inv, tiled;
+  const PassDesc* passes;  // forward order
+  int npasses;
+  size_t batch;
+};
+
+rg_status ntt_run_L1(const NttLaunch& p, hipStream_t st);
+rg_status ntt_run_L2(const NttLaunch& p, hipStream_t st);
+rg_status ntt_run_L4(const NttLaunch& p, hipStream_t st);
+rg_status ntt_run_L7(const NttLaunch& p, hipStream_t st);
+rg_status ntt_run_L14(const NttLaunch& p, hipStream_t st);
+
+}  // namespace rg
