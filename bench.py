@@ -1,0 +1,222 @@
+"""bench.py -- NTT / Jindo-commit throughput of libringo on MI355X.
+
+Contract (see task): `python bench.py --gpus N --steps K --warmup W`; for N > 1 it is launched
+by torch.distributed.run, one rank per GPU (RCCL).  Rank 0 prints ONE JSON line.
+
+Headline (BASELINE.json configs[1]): forward + inverse negacyclic NTT, degree 2^16, the single
+63-bit jindo-modulus prime p = 47104^4 + 1, batch 1024 polynomials per GPU, inputs resident in
+HBM.  One step = FwdNTTTo then InvNTTTo over the whole batch (2048 transforms).  Unit: NTTs/s
+(one forward or one inverse transform of one polynomial), whole job.  Scaling: weak (each rank
+owns its own 1024 polys; no data-path collective).
+
+Secondary lines in the same JSON object (also measured, not the headline value):
+  * l4_ntt: the same fwd+inv step at the Jindo default 255-bit prime (configs[3]), batch 64
+  * jindo: device-resident Jindo commits/s at targetN 2^14 (configs[2]) when available
+
+roofline: for the NTT transform (two LDS-tiled pass kernels per chunk of polys): algorithmic
+bytes = one read + one write of N*8 B per polynomial per transform; achieved = those bytes /
+the transform's duration measured with HIP events on the launch stream over the timed region.
+cpu_baseline: the C restatement (oracle/liboracle.so, OpenMP) timed on this host on a bounded
+sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ringo-snark_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+P63 = 47104 ** 4 + 1
+Q255 = 0x430D45996B62AFC2D65643D9E6FB65558E9630DC8C3732810000000000000001
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def splitmix64(seed, n):
+    """SplitMix64 stream (SURVEY.md §8d synthetic inputs), vectorised in numpy."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def uniform_elems(q, L, n, seed):
+    """n uniform residues in [0, q) as [n][L] limbs.  The Montgomery map is a bijection on
+    [0, q), so these are also uniform Montgomery representations."""
+    if L == 1:
+        v = splitmix64(seed, n)
+        return (v % np.uint64(q)).reshape(n, 1)
+    w = splitmix64(seed, n * L).reshape(n, L)
+    top = (q >> (64 * (L - 1))).bit_length()
+    w[:, L - 1] &= np.uint64((1 << max(top - 1, 1)) - 1)  # < 2^(bits-1) <= q: in range
+    return w
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--logn", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the L=4 / Jindo lines")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+class Events:
+    """HIP-event timing of calls on one stream (the stream the kernels are launched on)."""
+
+    def __init__(self, torch, stream):
+        self.torch, self.stream, self.pairs = torch, stream, []
+
+    def time(self, fn):
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record(self.stream)
+        fn()
+        e1.record(self.stream)
+        self.pairs.append((e0, e1))
+
+    def total_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.pairs)
+
+
+def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
+    N = 1 << logn
+    dev = torch.device("cuda", torch.cuda.current_device())
+    F = ringo.Field(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    host = uniform_elems(q, L, batch * N, seed)
+    x = torch.from_numpy(host.view(np.int64).reshape(-1)).to(dev)
+    ref = x.clone()
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is None:
+            T.fwd_dev(x, x, batch, stream)
+            T.inv_dev(x, x, batch, stream)
+        else:
+            ev.time(lambda: T.fwd_dev(x, x, batch, stream))
+            ev.time(lambda: T.inv_dev(x, x, batch, stream))
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = Events(torch, stream)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(ev)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ok = bool(torch.equal(x, ref))  # fwd then inv is the identity: full-size self-check
+    kern_ms = ev.total_ms()
+    return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L)
+
+
+def cpu_baseline(q, L, logn, seconds):
+    """C restatement (oracle/liboracle.so) fwd+inv on this host: bounded sample, all threads
+    the OpenMP runtime gives it (OMP_NUM_THREADS)."""
+    import coracle as co
+    cf = co.CField(q)
+    N = 1 << logn
+    tw, twi, ninv = cf.tables(N)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    chunk = max(threads, 1)
+    a = uniform_elems(q, L, chunk * N, 0x52494E47).reshape(chunk, N, L)
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        y = cf.ntt_fwd(a, tw)
+        cf.ntt_inv(y, twi, ninv)
+        done += 2 * chunk
+    el = time.perf_counter() - t0
+    return dict(value=done / el, unit="NTT/s", cores=threads, kind="port",
+                sample=f"{done} transforms (fwd+inv pairs of {chunk} polys, N=2^{logn}, L={L}) in {el:.1f} s "
+                       "by oracle/oracle.c (C restatement of ntt.go; Go toolchain absent on this host)")
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+    torch.cuda.set_device(local)
+    import ringo
+
+    ringo.lib().rg_set_device(local)
+    r = ntt_step_bench(torch, ringo, dist, P63, 1, args.batch, args.logn, args.steps, args.warmup,
+                       0x52494E47 + rank)
+    ms_step = r["wall_s"] * 1000.0 / args.steps
+    if dist is not None:
+        t = torch.tensor([ms_step, r["kernel_ms"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms_step, kern_ms = float(t[0]), float(t[1])
+        okt = torch.tensor([0 if r["ok"] else 1], device="cuda")
+        dist.all_reduce(okt)
+        ok = int(okt.item()) == 0
+    else:
+        kern_ms, ok = r["kernel_ms"], r["ok"]
+    value = world * 2 * args.batch / (ms_step / 1000.0)
+    N = 1 << args.logn
+    bytes_per_ntt = 2 * N * 8
+    achieved = bytes_per_ntt * r["ntts"] / (kern_ms / 1000.0) / 1e9
+    out = {
+        "metric": "NTTs/sec (fwd+inv negacyclic, degree 2^16, 63-bit prime, batch 1024/GPU)",
+        "value": value,
+        "unit": "NTT/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (SplitMix64 seed 0x52494E47, uniform residues mod p)",
+        "config": {"workload": "configs[1]: fwd+inv negacyclic NTT, N=2^16, p=47104^4+1 (63-bit), "
+                               f"batch {args.batch} polys per GPU, HBM-resident",
+                   "rank": N, "field_bits": 63, "batch_per_gpu": args.batch, "parallelism": f"replicas x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "NTT transform = 2 LDS-tiled pass kernels (ntt_pass_kernel<1,8,..>) per chunk",
+                     "bytes_per_unit": bytes_per_ntt},
+        "selfcheck_fwd_inv_identity": ok,
+    }
+    if not args.no_extra:
+        r4 = ntt_step_bench(torch, ringo, dist, Q255, 4, 64, args.logn, max(2, args.steps // 2), 1, 7 + rank)
+        ms4 = r4["wall_s"] * 1000.0 / max(2, args.steps // 2)
+        out["l4_ntt"] = {"value": world * 2 * 64 / (ms4 / 1000.0), "unit": "NTT/s",
+                         "config": "configs[3]: fwd+inv negacyclic NTT, N=2^16, 255-bit Jindo prime, batch 64/GPU",
+                         "achieved_GBs": 2 * N * 32 * r4["ntts"] / (r4["kernel_ms"] / 1000.0) / 1e9,
+                         "selfcheck_fwd_inv_identity": r4["ok"]}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(P63, 1, args.logn, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,7 @@
 //   sees ~one read and one write per element per transform.
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -47,6 +48,7 @@ struct NttArgs {
   uint64_t w1n[L];   // twInv[1] * N^-1
   uint64_t w1n_sh;
   int logN, G0;
+  int qlo1;             // q mod 2^32 == 1 (L == 1 fast reduction)
   long long total_sub;  // batch * N / 2^P
 };
 
@@ -118,6 +120,112 @@ __device__ __forceinline__ void bfly_inv(uint64_t* u, uint64_t* v, const Tw<L, S
 }
 
 __device__ __forceinline__ int padx(int x) { return x + (x >> 4); }
+
+// ----------------------------------------------------------------------------------------
+// Lock-step single-word Shoup stages (L = 1).  One radix-2 stage of a radix-16 round is 8
+// independent butterflies; writing each micro-step for all 8 before the next one exposes
+// 8-way ILP in program order, which hides the dependent-issue latency and the carry/VCC
+// hazards of 64-bit integer code at the low occupancy the register-resident tile allows.
+// q < 2^63 (checked at plan creation) so every intermediate fits one word.
+// ----------------------------------------------------------------------------------------
+struct ShoupK {
+  uint64_t q;
+  uint32_t qlo1;  // q mod 2^32 == 1  ->  lo64(x*q) = x + ((x_lo*q_hi) << 32)
+};
+
+__device__ __forceinline__ uint64_t lo64_mul_q(uint64_t x, uint64_t q, bool qlo1) {
+  if (qlo1) {
+    const uint32_t m = (uint32_t)x * (uint32_t)(q >> 32);
+    return x + ((uint64_t)m << 32);
+  }
+  return x * q;
+}
+
+// 32-bit-half arithmetic with explicit carry chains: the borrow out of the trial
+// subtraction IS the select mask (no separate 64-bit compare), q < 2^63.
+__device__ __forceinline__ uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ __forceinline__ uint64_t addmod63(uint64_t a, uint64_t b, uint64_t q) {
+  uint32_t c, br;
+  const uint32_t s0 = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c);
+  const uint32_t s1 = __builtin_addc((uint32_t)(a >> 32), (uint32_t)(b >> 32), c, &c);
+  const uint32_t t0 = __builtin_subc(s0, (uint32_t)q, 0u, &br);
+  const uint32_t t1 = __builtin_subc(s1, (uint32_t)(q >> 32), br, &br);
+  return br ? pack(s0, s1) : pack(t0, t1);
+}
+__device__ __forceinline__ uint64_t submod63(uint64_t a, uint64_t b, uint64_t q) {
+  uint32_t br, c;
+  const uint32_t d0 = __builtin_subc((uint32_t)a, (uint32_t)b, 0u, &br);
+  const uint32_t d1 = __builtin_subc((uint32_t)(a >> 32), (uint32_t)(b >> 32), br, &br);
+  const uint32_t e0 = __builtin_addc(d0, (uint32_t)q, 0u, &c);
+  const uint32_t e1 = __builtin_addc(d1, (uint32_t)(q >> 32), c, &c);
+  return br ? pack(e0, e1) : pack(d0, d1);
+}
+__device__ __forceinline__ uint64_t reduce2q(uint64_t r, uint64_t q) {  // [0, 2q) -> [0, q)
+  uint32_t br;
+  const uint32_t t0 = __builtin_subc((uint32_t)r, (uint32_t)q, 0u, &br);
+  const uint32_t t1 = __builtin_subc((uint32_t)(r >> 32), (uint32_t)(q >> 32), br, &br);
+  return br ? r : pack(t0, t1);
+}
+// y * w mod q (Shoup, w' = floor(w 2^64 / q)), result in [0, 2q)
+template <bool QLO1>
+__device__ __forceinline__ uint64_t shoup_lazy(uint64_t y, uint64_t w, uint64_t wp, uint64_t q) {
+  const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
+  const uint32_t p0 = (uint32_t)wp, p1 = (uint32_t)(wp >> 32);
+  const uint64_t t1 = mad64(y1, p0, __umulhi(y0, p0));
+  const uint64_t t2 = mad64(y0, p1, (uint32_t)t1);
+  const uint64_t qh = mad64(y1, p1, t1 >> 32) + (t2 >> 32);
+  const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+  const uint64_t pw = mad64(y0, w0, 0);
+  const uint32_t yw1 = (uint32_t)(pw >> 32) + y0 * w1 + y1 * w0;
+  const uint32_t yw0 = (uint32_t)pw;
+  if constexpr (QLO1) {
+    const uint32_t m = (uint32_t)qh * (uint32_t)(q >> 32);
+    uint32_t br;
+    const uint32_t r0 = __builtin_subc(yw0, (uint32_t)qh, 0u, &br);
+    const uint32_t r1 = __builtin_subc(yw1, (uint32_t)(qh >> 32), br, &br) - m;
+    return pack(r0, r1);
+  } else {
+    return pack(yw0, yw1) - qh * q;
+  }
+}
+
+// fwd: for k in [0, 8): (u_k, v_k) <- (u_k + w_k v_k, u_k - w_k v_k); twiddle w_k = tw[k / HALF]
+template <int HALF, bool QLO1>
+__device__ __forceinline__ void stage8_fwd(uint64_t (&e)[16][1], const uint64_t* w, const uint64_t* wp, uint64_t q) {
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int blk = k / HALF, u = k % HALF, i1 = blk * 2 * HALF + u + HALF;
+    r[k] = shoup_lazy<QLO1>(e[i1][0], w[blk], wp[blk], q);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = reduce2q(r[k], q);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int blk = k / HALF, u = k % HALF, i0 = blk * 2 * HALF + u, i1 = i0 + HALF;
+    const uint64_t a = e[i0][0];
+    e[i0][0] = addmod63(a, r[k], q);
+    e[i1][0] = submod63(a, r[k], q);
+  }
+}
+
+// inv: (u, v) <- (u + v, (u - v) w)
+template <int HALF, bool QLO1>
+__device__ __forceinline__ void stage8_inv(uint64_t (&e)[16][1], const uint64_t* w, const uint64_t* wp, uint64_t q) {
+  uint64_t d[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int blk = k / HALF, u = k % HALF, i0 = blk * 2 * HALF + u, i1 = i0 + HALF;
+    const uint64_t a = e[i0][0], b = e[i1][0];
+    e[i0][0] = addmod63(a, b, q);
+    d[k] = submod63(a, b, q);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int blk = k / HALF, u = k % HALF, i1 = blk * 2 * HALF + u + HALF;
+    e[i1][0] = reduce2q(shoup_lazy<QLO1>(d[k], w[blk], wp[blk], q), q);
+  }
+}
 
 // ----------------------------------------------------------------------------------------
 // rounds
@@ -389,6 +497,7 @@ static void fill_args(NttArgs<L>& a, const NttLaunch& p) {
   a.w1n_sh = p.w1n_sh;
   a.logN = p.logN;
   a.tw = p.tw;
+  a.qlo1 = (uint32_t)p.q[0] == 1u;
 }
 
 template <int L, int P, bool INV, bool SHOUP, bool SCALE>
@@ -419,6 +528,317 @@ static rg_status dispatch_P(int p, const NttArgs<L>& a, hipStream_t st) {
   }
 }
 
+}  // namespace rg
+
+// ----------------------------------------------------------------------------------------
+// 2-round pass specialisation (P = 8 = 2 x radix-16), the shape of every pass of the
+// degree-2^16 transform.  Compared with ntt_pass_kernel:
+//   * global <-> VGPR directly wherever the round's point pattern is coalesced (column
+//     passes always; row passes on the side where lanes walk consecutive x), so LDS carries
+//     only the one exchange between the rounds (plus one transpose on the row pass's other
+//     side);
+//   * persistent workgroups: the next tile's global loads are issued before the current
+//     tile's butterflies, hiding HBM latency under VALU work (L = 1);
+//   * twiddles that are uniform over the workgroup (column pass, the high-bit round) come
+//     from scalar loads.
+// Lane mapping: COL: s = tid & 15 (column, consecutive addresses), t = tid >> 4;
+//               ROW: t = tid & 15 (consecutive addresses), s = tid >> 4.
+// LDS layout lds[l][s * PADN + pad(x)]: COL uses pad(x) = x, PADN = 257; ROW uses
+// pad(x) = x + x/16, PADN = 272 (see DESIGN.md for the bank analysis).
+// ----------------------------------------------------------------------------------------
+namespace rg {
+
+template <bool COL>
+struct R2Layout {
+  static constexpr int PADN = COL ? 257 : 272;
+  __device__ static __forceinline__ int pad(int x) { return COL ? x : x + (x >> 4); }
+};
+
+template <int L, bool SHOUP, bool UNIFORM>
+__device__ __forceinline__ void load_tw2(Tw<L, SHOUP>& w, const uint64_t* tw, long long idx) {
+  if constexpr (UNIFORM) {
+    const int i = __builtin_amdgcn_readfirstlane((int)idx);
+    load_tw<L, SHOUP>(w, tw, i);
+  } else {
+    load_tw<L, SHOUP>(w, tw, idx);
+  }
+}
+
+
+template <int SP, bool INV, bool SCALE, bool QLO1>
+__device__ __forceinline__ void lockstep_stage(const NttArgs<1>& a, uint64_t (&e)[16][1], bool high, long long hi,
+                                               int o_high, bool uniform) {
+  // forward stage SP of the round: HALF = 8 >> SP, 2^SP twiddles; inverse: HALF = 1 << SP
+  constexpr int HALF = INV ? (1 << SP) : (8 >> SP);
+  constexpr int NB = 8 / HALF;
+  const int gp = INV ? (7 - ((high ? 4 : 0) + SP)) : ((high ? 0 : 4) + SP);
+  const int shift = INV ? (3 - SP) : SP;
+  uint64_t w[NB], wp[NB];
+  const bool last = INV && SCALE && (a.G0 + gp == 0);
+  if (last) {
+    w[0] = a.w1n[0];
+    wp[0] = a.w1n_sh;
+  } else {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      long long idx = (1LL << (a.G0 + gp)) + (hi << gp) + ((long long)o_high << shift) + b;
+      if (uniform) idx = __builtin_amdgcn_readfirstlane((int)idx);
+      const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[idx];
+      w[b] = v.x;
+      wp[b] = v.y;
+    }
+  }
+  const uint64_t q = a.F.q[0];
+  if constexpr (!INV) {
+    stage8_fwd<HALF, QLO1>(e, w, wp, q);
+  } else {
+    stage8_inv<HALF, QLO1>(e, w, wp, q);
+    if (last) {  // (u + v) * N^-1 on the 8 upper outputs
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i0 = (k / HALF) * 2 * HALF + (k % HALF);
+        e[i0][0] = shoup_mul(e[i0][0], a.nsc[0], a.nsc_sh, q);
+      }
+    }
+  }
+}
+
+template <bool INV, bool SCALE, bool QLO1>
+__device__ __forceinline__ void lockstep_round(const NttArgs<1>& a, uint64_t (&e)[16][1], bool high, long long hi,
+                                               int o_high, bool uniform) {
+  lockstep_stage<0, INV, SCALE, QLO1>(a, e, high, hi, o_high, uniform);
+  lockstep_stage<1, INV, SCALE, QLO1>(a, e, high, hi, o_high, uniform);
+  lockstep_stage<2, INV, SCALE, QLO1>(a, e, high, hi, o_high, uniform);
+  lockstep_stage<3, INV, SCALE, QLO1>(a, e, high, hi, o_high, uniform);
+}
+
+template <int L, bool INV, bool SHOUP, bool SCALE, bool COL, bool PREFETCH, bool QLO1>
+__global__ __launch_bounds__(kWG) void ntt_r2_kernel(NttArgs<L> a) {
+  constexpr int NP = 256, SW = 16;
+  using LY = R2Layout<COL>;
+  constexpr int PADN = LY::PADN;
+  __shared__ uint64_t lds[L * SW * PADN];
+
+  const int tid = threadIdx.x;
+  const int s = COL ? (tid & 15) : (tid >> 4);
+  const int t = COL ? (tid >> 4) : (tid & 15);
+  const int logN = a.logN;
+  const int logS = logN - a.G0 - 8;  // COL: logS >= 4; ROW: 0
+  const long long ntiles = a.total_sub / SW;
+  const int rowshift = logN - a.G0;
+
+  // Addressing: a tile-uniform base (SGPRs) plus a 32-bit per-lane element offset, so the
+  // loads/stores use saddr + voffset and no 64-bit address is kept per point.
+  //   COL: elem = (rowid0 << rowshift) + lo0 + (x << logS) + s
+  //   ROW: elem = (sub0 << rowshift) + (s << rowshift) + x
+  auto tile_base = [&](long long tile) -> long long {
+    const long long sub0 = tile * SW;
+    if constexpr (COL)
+      return ((sub0 >> logS) << rowshift) + (sub0 & ((1LL << logS) - 1));
+    else
+      return sub0 << rowshift;
+  };
+  const uint32_t lane_off = COL ? (uint32_t)s : ((uint32_t)s << rowshift);
+  const int xshift = COL ? logS : 0;
+  auto gload = [&](uint64_t (&r)[16][L], long long tile, bool low_pattern) {
+    const uint64_t* base = a.in + tile_base(tile) * L;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      const uint32_t x = low_pattern ? (16 * t + y) : (t + 16 * y);
+      const uint32_t off = ((x << xshift) + lane_off) * L;
+#pragma unroll
+      for (int l = 0; l < L; ++l) r[y][l] = base[off + l];
+    }
+  };
+  auto gstore = [&](const uint64_t (&r)[16][L], long long tile, bool low_pattern) {
+    uint64_t* base = a.out + tile_base(tile) * L;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      const uint32_t x = low_pattern ? (16 * t + y) : (t + 16 * y);
+      const uint32_t off = ((x << xshift) + lane_off) * L;
+#pragma unroll
+      for (int l = 0; l < L; ++l) base[off + l] = r[y][l];
+    }
+  };
+  auto lds_put = [&](const uint64_t (&r)[16][L], bool low_pattern) {
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      const int x = low_pattern ? (16 * t + y) : (t + 16 * y);
+#pragma unroll
+      for (int l = 0; l < L; ++l) lds[l * SW * PADN + s * PADN + LY::pad(x)] = r[y][l];
+    }
+  };
+  auto lds_get = [&](uint64_t (&r)[16][L], bool low_pattern) {
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      const int x = low_pattern ? (16 * t + y) : (t + 16 * y);
+#pragma unroll
+      for (int l = 0; l < L; ++l) r[y][l] = lds[l * SW * PADN + s * PADN + LY::pad(x)];
+    }
+  };
+
+  // radix-16 round on e[y] (y = the 4 bits being transformed), forward (DIT, top bit first)
+  // or inverse (DIF, low bit first).  `high` selects the x-bit window [4,8) vs [0,4).
+  auto round = [&](uint64_t (&e)[16][L], bool high, long long hi) {
+    // o_high: bits of x above the window (t when the window is [0,4), none otherwise)
+    const int o_high = high ? 0 : t;
+    const bool uniform = COL && high;  // twiddle index depends on nothing per-lane
+    if constexpr (L == 1 && SHOUP) {
+      lockstep_round<INV, SCALE, QLO1>(a, e, high, hi, o_high, uniform);
+      return;
+    }
+    if constexpr (!INV) {
+#pragma unroll
+      for (int sp = 0; sp < 4; ++sp) {
+        const int gp = (high ? 0 : 4) + sp;
+        const int half = 8 >> sp;
+#pragma unroll
+        for (int blk = 0; blk < (1 << sp); ++blk) {
+          const long long idx = (1LL << (a.G0 + gp)) + (hi << gp) + ((long long)o_high << sp) + blk;
+          Tw<L, SHOUP> w;
+          if (uniform)
+            load_tw2<L, SHOUP, true>(w, a.tw, idx);
+          else
+            load_tw2<L, SHOUP, false>(w, a.tw, idx);
+#pragma unroll
+          for (int u = 0; u < half; ++u) {
+            const int i0 = blk * 2 * half + u;
+            bfly_fwd<L, SHOUP>(e[i0], e[i0 + half], w, a.F);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int sp = 0; sp < 4; ++sp) {
+        const int lo = high ? 4 : 0;
+        const int gp = 7 - (lo + sp);
+        const int half = 1 << sp;
+        const bool last = SCALE && (a.G0 + gp == 0);
+#pragma unroll
+        for (int blk = 0; blk < (16 >> (sp + 1)); ++blk) {
+          const long long idx = (1LL << (a.G0 + gp)) + (hi << gp) + ((long long)o_high << (3 - sp)) + blk;
+          Tw<L, SHOUP> w;
+          if (last) {
+#pragma unroll
+            for (int l = 0; l < L; ++l) w.w[l] = a.w1n[l];
+            w.wp = a.w1n_sh;
+          } else if (uniform) {
+            load_tw2<L, SHOUP, true>(w, a.tw, idx);
+          } else {
+            load_tw2<L, SHOUP, false>(w, a.tw, idx);
+          }
+#pragma unroll
+          for (int u = 0; u < half; ++u) {
+            const int i0 = blk * 2 * half + u;
+            bfly_inv<L, SHOUP>(e[i0], e[i0 + half], w, a.F);
+            if (last) {
+              Tw<L, SHOUP> ns;
+#pragma unroll
+              for (int l = 0; l < L; ++l) ns.w[l] = a.nsc[l];
+              ns.wp = a.nsc_sh;
+              uint64_t z[L];
+              mul_tw<L, SHOUP>(z, e[i0], ns, a.F);
+#pragma unroll
+              for (int l = 0; l < L; ++l) e[i0][l] = z[l];
+            }
+          }
+        }
+      }
+    }
+  };
+
+  // forward: round A = high window (pattern x = t + 16y), round B = low window (x = 16t + y)
+  // inverse: round A = low window, round B = high window
+  const bool a_low = INV;
+  uint64_t cur[16][L], nxt[16][L];
+  long long tile = blockIdx.x;
+  // ROW + first round on the low pattern: lanes walk x = 16t+y -> load coalesced (x = t+16y)
+  // and transpose through LDS.
+  constexpr bool LOAD_T = !COL && INV;
+  constexpr bool STORE_T = !COL && !INV;
+  if (tile < ntiles) gload(cur, tile, LOAD_T ? false : a_low);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const long long nt = tile + gridDim.x;
+    if (PREFETCH && nt < ntiles) gload(nxt, nt, LOAD_T ? false : a_low);
+    const long long hi = COL ? 0 : ((tile * SW + s) & ((1LL << a.G0) - 1));
+    if constexpr (LOAD_T) {
+      lds_put(cur, false);
+      __syncthreads();
+      lds_get(cur, true);
+      __syncthreads();
+    }
+    round(cur, !a_low, hi);
+    lds_put(cur, a_low);
+    __syncthreads();
+    lds_get(cur, !a_low);
+    __syncthreads();
+    round(cur, a_low, hi);
+    if constexpr (STORE_T) {
+      lds_put(cur, true);
+      __syncthreads();
+      lds_get(cur, false);
+      __syncthreads();
+      gstore(cur, tile, false);
+    } else {
+      gstore(cur, tile, !a_low);
+    }
+    if (PREFETCH) {
+#pragma unroll
+      for (int y = 0; y < 16; ++y)
+#pragma unroll
+        for (int l = 0; l < L; ++l) cur[y][l] = nxt[y][l];
+    } else if (nt < ntiles) {
+      gload(cur, nt, LOAD_T ? false : a_low);
+    }
+  }
+}
+
+template <int L, bool INV, bool SHOUP, bool SCALE, bool COL, bool PF, bool QLO1>
+static rg_status launch_r2_pf(const NttArgs<L>& a, hipStream_t st) {
+  const long long ntiles = a.total_sub / 16;
+  static int grid_cap = 0;
+  if (!grid_cap) {
+    int per_cu = 0, dev = 0, cus = 256;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ntt_r2_kernel<L, INV, SHOUP, SCALE, COL, PF, QLO1>, kWG, 0);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid_cap = (per_cu > 0 ? per_cu : 1) * cus;
+  }
+  const long long grid = ntiles < grid_cap ? ntiles : grid_cap;
+  hipLaunchKernelGGL((ntt_r2_kernel<L, INV, SHOUP, SCALE, COL, PF, QLO1>), dim3((unsigned)grid), dim3(kWG), 0, st, a);
+  return check_launch("ntt_r2");
+}
+
+// RINGO_NTT_PREFETCH=0 disables the next-tile register prefetch (A/B switch for tuning)
+static inline bool r2_prefetch_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RINGO_NTT_PREFETCH");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+template <int L, bool INV, bool SHOUP, bool SCALE, bool COL>
+static rg_status launch_r2(const NttArgs<L>& a, hipStream_t st) {
+  const bool pf = L == 1 && r2_prefetch_enabled();
+  if (L == 1 && SHOUP && a.qlo1) {
+    if (pf) return launch_r2_pf<L, INV, SHOUP, SCALE, COL, true, true>(a, st);
+    return launch_r2_pf<L, INV, SHOUP, SCALE, COL, false, true>(a, st);
+  }
+  if (pf) return launch_r2_pf<L, INV, SHOUP, SCALE, COL, true, false>(a, st);
+  return launch_r2_pf<L, INV, SHOUP, SCALE, COL, false, false>(a, st);
+}
+
+template <int L, bool INV, bool SHOUP, bool SCALE>
+static rg_status dispatch_r2(bool col, const NttArgs<L>& a, hipStream_t st) {
+  return col ? launch_r2<L, INV, SHOUP, SCALE, true>(a, st) : launch_r2<L, INV, SHOUP, SCALE, false>(a, st);
+}
+
+}  // namespace rg
+
+namespace rg {
+
 template <int L, bool SHOUP>
 static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
   const size_t N = (size_t)1 << p.logN;
@@ -437,6 +857,19 @@ static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
       a.G0 = ps.G0;
       a.total_sub = (long long)nb * (long long)(N >> ps.P);
       rg_status s;
+      // 2-round specialisation: P = 8 with radix 16, column pass (stride >= 16) or row pass
+      const int logS = p.logN - ps.G0 - ps.P;
+      if (RadixOf<L>::value == 4 && ps.P == 8 && (logS == 0 || logS >= 4) && (a.total_sub % 16) == 0) {
+        const bool col = logS >= 4;
+        if (!p.inv)
+          s = dispatch_r2<L, false, SHOUP, false>(col, a, st);
+        else if (ps.G0 == 0)
+          s = dispatch_r2<L, true, SHOUP, true>(col, a, st);
+        else
+          s = dispatch_r2<L, true, SHOUP, false>(col, a, st);
+        RG_TRY(s);
+        continue;
+      }
       if (!p.inv)
         s = dispatch_P<L, false, SHOUP, false>(ps.P, a, st);
       else if (ps.G0 == 0)
@@ -474,3 +907,4 @@ static rg_status run_stages(const NttLaunch& p, hipStream_t st) {
 }
 
 }  // namespace rg
+
