@@ -1,11 +1,1029 @@
-// jindo.hip -- placeholder (commit pipeline lands next)
+// jindo.hip -- the Jindo commitment (jindo/prover.go:45-202) on gfx950, batched over
+// independent commits, with the prover's randomness injected (include/ringo.h).
+//
+// Pipeline per batch of B commits (all device-resident, one stream):
+//   1. digits_kernel   thread per (commit, column, row, slot): source element (v, firstRow =
+//                      v - lastRow shifted, lastRow, mask; prover.go:65-128) -> fromMont ->
+//                      base-b digits (encoder.go:120-146, utils.go:12-19) into the encode's
+//                      coefficient slots j*slots+i.
+//   2. prep_kernel     workgroup per ring polynomial: the randEncode tail (encoder.go:166-200:
+//                      MForm(noise), X^slots negacyclic shift, - b*s, + MForm(digits)) or the
+//                      MLWE finalize (prover.go:130-141: signed residue, MForm), then the
+//                      d-point negacyclic NTT per RNS limb in LDS (Lattigo ordering/roots).
+//   3. mac_kernel      thread per (commit, column, limb, coeff): the inner Ajtai product
+//                      sum_k In[j][k]*Enc[k] + sum_k CK.MLWE[j][k]*MLWE[k] for every j, kept
+//                      as exact 160-bit sums and reduced once (MulCoeffsMontgomeryThenAdd
+//                      summed == (sum a*b) * 2^-64 mod q), + MLWE[mlwe+j] (prover.go:149-157).
+//   4. round_kernel    workgroup per polynomial: IMForm, INTT, centred CRT (Garner, up to 4
+//                      primes), floor shift by the cut, Euclidean mod q', MForm, NTT in the
+//                      destination ring (prover.go:164-176, rns.go:76-114).
+//   5. mac_kernel + round_kernel again for the outer commitment (prover.go:180-202).
+// All residues are canonical, so results are bit-exact against the reference's Lattigo
+// calls given the same primes (Lattigo conventions restated: see DESIGN.md, "parity").
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ck_crs.hpp"
 #include "common.hpp"
-extern "C" {
-rg_status rg_jindo_create(const rg_jindo_params*, const uint64_t*, const uint64_t*, const uint64_t*, rg_jindo**) { return RG_ERR_UNSUPPORTED; }
-rg_status rg_jindo_create_from_crs(const rg_jindo_params*, const uint8_t*, size_t, rg_jindo**) { return RG_ERR_UNSUPPORTED; }
-void rg_jindo_destroy(rg_jindo*) {}
-rg_status rg_jindo_commit_key(const rg_jindo*, uint64_t*, uint64_t*, uint64_t*) { return RG_ERR_UNSUPPORTED; }
-rg_status rg_jindo_commit(const rg_jindo*, const uint64_t*, size_t, const uint64_t*, const uint64_t*, const int64_t*, const int64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*) { return RG_ERR_UNSUPPORTED; }
-rg_status rg_jindo_commit_dev(const rg_jindo*, size_t, const uint64_t*, size_t, const uint64_t*, const uint64_t*, const int64_t*, const int64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, void*) { return RG_ERR_UNSUPPORTED; }
-size_t rg_jindo_scratch_bytes(const rg_jindo*, size_t) { return 0; }
+#include "field.hpp"
+#include "host_field.hpp"
+
+namespace rg {
+
+constexpr int kMaxQ = 4;     // RNS limbs per ring
+constexpr int kMaxD = 1024;  // ring degree supported by the LDS kernels
+constexpr int kMaxJ = 32;    // MSIS rank accumulated per thread
+
+struct RnsPrime {
+  uint64_t q;
+  uint64_t rinv, rinv_sh;    // 2^-64 mod q (IMForm)
+  uint64_t r64, r64_sh;      // 2^64 mod q (MForm)
+  uint64_t one_sh;           // floor(2^64 / q): x mod q = shoup(x, 1)
+  uint64_t ninv, ninv_sh;    // d^-1 mod q
+  uint64_t bmod, bmod_sh;    // base mod q
+};
+
+struct RingDev {
+  int n;                    // limbs
+  RnsPrime p[kMaxQ];
+  const ulonglong2* fwd;    // [n][d] (w, w') psi^brv
+  const ulonglong2* bwd;    // [n][d] psi^-brv
+};
+
+// CRT (Garner) constants for a source ring
+struct CrtDev {
+  int n;
+  uint64_t q[kMaxQ];
+  uint64_t inv[kMaxQ][kMaxQ], inv_sh[kMaxQ][kMaxQ];  // inv[j][k] = q_k^-1 mod q_j (k < j)
+  uint64_t Q[4], Qhalf[4];                            // product (4 words) and floor(Q/2)
+};
+
+// destination mod constants: 2^(64k) mod q' for multiword reduction
+struct DstDev {
+  int n;
+  uint64_t pw[kMaxQ][4], pw_sh[kMaxQ][4];
+};
+
+// ------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t sh_mul(uint64_t y, uint64_t w, uint64_t wp, uint64_t q) {
+  return shoup_mul(y, w, wp, q);
 }
+__device__ __forceinline__ uint64_t signed_residue(long long c, uint64_t q) {
+  // setCoeffSigned (utils.go:49-61): c >= 0 -> c ; else Go's c%q + q (== q when q | c; the
+  // following MForm maps that to 0 either way)
+  if (c >= 0) return (uint64_t)c % q;
+  const uint64_t a = (uint64_t)(-(c + 1)) + 1;
+  return q - a % q;
+}
+
+// d-point negacyclic NTT (Lattigo ordering: natural -> bit-reversed) of one limb held in LDS,
+// by `nt` threads (thread index `ti`); synchronises the whole workgroup between stages.
+__device__ void ntt_lds(uint64_t* p, int d, const ulonglong2* roots, uint64_t q, int ti, int nt, bool active) {
+  for (int m = 1, t = d >> 1; m < d; m <<= 1, t >>= 1) {
+    if (active) {
+      for (int k = ti; k < (d >> 1); k += nt) {
+        const int i = k / t, j = 2 * i * t + (k % t);
+        const ulonglong2 w = roots[m + i];
+        const uint64_t u = p[j], v = sh_mul(p[j + t], w.x, w.y, q);
+        p[j] = mod_add(u, v, q);
+        p[j + t] = mod_sub(u, v, q);
+      }
+    }
+    __syncthreads();
+  }
+}
+// inverse (GS, bit-reversed -> natural), times d^-1
+__device__ void intt_lds(uint64_t* p, int d, const ulonglong2* roots, const RnsPrime& P, int ti, int nt, bool active) {
+  const uint64_t q = P.q;
+  for (int m = d >> 1, t = 1; m >= 1; m >>= 1, t <<= 1) {
+    if (active) {
+      for (int k = ti; k < (d >> 1); k += nt) {
+        const int i = k / t, j = 2 * i * t + (k % t);
+        const ulonglong2 w = roots[m + i];
+        const uint64_t u = p[j], v = p[j + t];
+        p[j] = mod_add(u, v, q);
+        p[j + t] = sh_mul(mod_sub(u, v, q), w.x, w.y, q);
+      }
+    }
+    __syncthreads();
+  }
+  if (active)
+    for (int k = ti; k < d; k += nt) p[k] = sh_mul(p[k], P.ninv, P.ninv_sh, q);
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. digits
+// ------------------------------------------------------------------------------------------
+struct JShape {
+  int rank, rows, cols, slots, exp, d, in_msis, out_msis, mlwe, dcmp, log_in_cut, log_out_cut;
+  int nq, nqo;
+  uint64_t base;
+  long long nv;
+};
+
+template <int L>
+struct DigitArgs {
+  JShape s;
+  FieldParams<L> F;
+  uint64_t base_inv;  // floor(2^64 / base)
+  const uint64_t* v;         // [B][nv][L]
+  const uint64_t* last_row;  // [B][cols*slots][L]
+  const uint64_t* mask;      // [B][rows][slots][L]
+  uint32_t* digits;          // [B][cols+1][rows][d]
+  long long total;           // B * (cols+1) * rows * slots
+};
+
+// (num = r * 2^32 + chunk) / b with the precomputed reciprocal, r < b < 2^32
+__device__ __forceinline__ uint32_t divstep(uint64_t num, uint64_t b, uint64_t binv, uint64_t& r) {
+  uint64_t qt = mul_hi(num, binv);
+  uint64_t rem = num - qt * b;
+  if (rem >= b) {
+    rem -= b;
+    ++qt;
+  }
+  r = rem;
+  return (uint32_t)qt;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
+  const JShape& S = a.s;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.total) return;
+  const int slot = (int)(gid % S.slots);
+  long long r = gid / S.slots;
+  const int row = (int)(r % S.rows);
+  r /= S.rows;
+  const int col = (int)(r % (S.cols + 1));
+  const long long b = r / (S.cols + 1);
+  const long long cs = (long long)S.cols * S.slots;
+  const uint64_t* vb = a.v + b * S.nv * L;
+  uint32_t* out = a.digits + (((b * (S.cols + 1) + col) * S.rows + row) * (long long)S.d);
+
+  // which element feeds this slot (prover.go:89-128); `have` = false -> zero slot
+  uint64_t x[L];
+  bool have = true;
+  if (col == S.cols) {  // mask column: every slot present
+    const uint64_t* m = a.mask + ((b * S.rows + row) * S.slots + slot) * L;
+#pragma unroll
+    for (int l = 0; l < L; ++l) x[l] = m[l];
+  } else if (row == S.rows - 1) {  // last row
+    const uint64_t* m = a.last_row + (b * cs + (long long)col * S.slots + slot) * L;
+#pragma unroll
+    for (int l = 0; l < L; ++l) x[l] = m[l];
+  } else if (row == 0) {  // first row: v[i] - lastRow[i-1] (genFirstLastRow :74-83)
+    const long long i = (long long)col * S.slots + slot;
+    uint64_t vi[L], lr[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) vi[l] = (i < S.nv) ? vb[i * L + l] : 0;
+    if (i == 0) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) x[l] = vi[l];
+    } else {
+      const uint64_t* m = a.last_row + (b * cs + i - 1) * L;
+#pragma unroll
+      for (int l = 0; l < L; ++l) lr[l] = m[l];
+      f_sub<L>(x, vi, lr, a.F);
+    }
+  } else {  // data row: v[row*cs + col*slots + slot] when < nv
+    const long long i = row * cs + (long long)col * S.slots + slot;
+    have = i < S.nv;
+#pragma unroll
+    for (int l = 0; l < L; ++l) x[l] = have ? vb[i * L + l] : 0;
+  }
+  // canonical limbs (Slice = fromMont)
+  uint64_t one[L], c[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) one[l] = (l == 0);
+  f_mul<L>(c, x, one, a.F);
+  if (!have) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) c[l] = 0;
+  }
+  // base-b digits: exp-1 remainders then the final quotient (encoder.go:125-136)
+  uint32_t w[2 * L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    w[2 * l] = (uint32_t)c[l];
+    w[2 * l + 1] = (uint32_t)(c[l] >> 32);
+  }
+  for (int jd = 0; jd < S.exp - 1; ++jd) {
+    uint64_t rem = 0;
+#pragma unroll
+    for (int k = 2 * L - 1; k >= 0; --k) w[k] = divstep((rem << 32) | w[k], S.base, a.base_inv, rem);
+    out[jd * S.slots + slot] = (uint32_t)rem;
+  }
+  out[(S.exp - 1) * S.slots + slot] = w[0];
+}
+
+// zero-fill digit slots not covered (d > exp*slots never happens for jindo; kept for safety)
+
+// ------------------------------------------------------------------------------------------
+// 2. prep: encode tail / MLWE finalize + NTT
+// ------------------------------------------------------------------------------------------
+struct PrepArgs {
+  JShape s;
+  RingDev R;
+  const uint32_t* digits;     // [B][cols+1][rows][d]
+  const long long* enc_noise;  // [B][cols+1][rows][d]
+  const long long* mlwe_noise; // [B][cols+1][nm][d]
+  const uint8_t* skip;         // [cols+1][rows] encodes the reference does not perform
+  uint64_t* enc;               // [B][cols+1][rows][nq][d]
+  uint64_t* mlwe;              // [B][cols+1][nm][nq][d]
+  long long n_enc;             // B * (cols+1) * rows
+};
+
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
+  __shared__ uint64_t poly[kMaxQ][kMaxD];
+  const JShape& S = a.s;
+  const int d = S.d, nq = S.nq, tid = threadIdx.x;
+  const int nm = S.in_msis + S.mlwe;
+  const long long job = blockIdx.x;
+  const bool is_enc = job < a.n_enc;
+  uint64_t* dst;
+  if (is_enc) {
+    const long long b = job / ((long long)(S.cols + 1) * S.rows);
+    const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
+    dst = a.enc + job * nq * d;
+    if (a.skip[cr]) {  // reference leaves Opening.Encode[i][j] at zero (prover.go:103-105,121-123)
+      for (int k = tid; k < nq * d; k += blockDim.x) dst[k] = 0;
+      return;
+    }
+    const uint32_t* dg = a.digits + job * d;
+    const long long* nz = a.enc_noise + job * d;
+    (void)b;
+    for (int k = tid; k < d; k += blockDim.x) {
+      const long long c = nz[k];
+      // the X^slots shift: coefficient k receives s[k - slots] (k >= slots) or -s[k + d - slots]
+      const int ks = k - S.slots;
+      const long long cs = ks >= 0 ? nz[ks] : nz[ks + d];
+      const uint64_t dgk = dg[k];
+      for (int l = 0; l < nq; ++l) {
+        const RnsPrime& P = a.R.p[l];
+        const uint64_t q = P.q;
+        const uint64_t sm = sh_mul(signed_residue(c, q), P.r64, P.r64_sh, q);    // MForm(s) :184
+        uint64_t sh = sh_mul(signed_residue(cs, q), P.r64, P.r64_sh, q);
+        if (ks < 0) sh = mod_neg(sh, q);  // wrapped coefficients negate (:191-195)
+        sh = mod_sub(sh, sh_mul(sm, P.bmod, P.bmod_sh, q), q);                   // :196
+        const uint64_t dm = sh_mul(dgk % q, P.r64, P.r64_sh, q);                 // MForm(digits) :198
+        poly[l][k] = mod_add(dm, sh, q);                                          // :199
+      }
+    }
+  } else {
+    const long long mj = job - a.n_enc;  // (b, col, j) flattened
+    dst = a.mlwe + mj * nq * d;
+    const long long* nz = a.mlwe_noise + mj * d;
+    for (int k = tid; k < d; k += blockDim.x) {
+      const long long c = nz[k];
+      for (int l = 0; l < nq; ++l) {
+        const RnsPrime& P = a.R.p[l];
+        poly[l][k] = sh_mul(signed_residue(c, P.q), P.r64, P.r64_sh, P.q);  // MForm (prover.go:140)
+      }
+    }
+    (void)nm;
+  }
+  __syncthreads();
+  // NTT per limb: two limbs at a time on the two halves of the workgroup
+  const int half = blockDim.x >> 1;
+  for (int l0 = 0; l0 < nq; l0 += 2) {
+    const int l = l0 + (tid >= half ? 1 : 0);
+    const bool active = l < nq;
+    const int lc = active ? l : l0;
+    ntt_lds(poly[lc], d, a.R.fwd + (long long)lc * d, a.R.p[lc].q, tid % half, half, active);
+  }
+  for (int k = tid; k < nq * d; k += blockDim.x) dst[k] = poly[k / d][k % d];
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. multiply-accumulate (inner / outer Ajtai products)
+// ------------------------------------------------------------------------------------------
+struct MacArgs {
+  int d, nl, J;            // degree, limbs, outputs per column
+  long long ncols;         // B * columns
+  int T1, T2;              // terms from operand set 1 / 2
+  const uint64_t* A1;      // [J][T1][nl][d]   commit key
+  const uint64_t* B1;      // [ncols][T1][nl][d] (stride b1_col per column, b1_term per term)
+  long long b1_col, b1_term;
+  const uint64_t* A2;      // [J][T2][nl][d]
+  const uint64_t* B2;
+  long long b2_col, b2_term;
+  const uint64_t* C;       // added after reduction: [ncols][...] + j * c_j  (nullable)
+  long long c_col, c_j;
+  uint64_t* out;           // [ncols][J][nl][d]
+  RnsPrime P[kMaxQ];
+};
+
+__device__ __forceinline__ void acc_add(uint64_t& lo, uint64_t& hi, uint32_t& top, uint64_t a, uint64_t b) {
+  uint64_t pl, ph;
+  mul_wide(a, b, pl, ph);
+  uint32_t c = 0;
+  lo = addc(lo, pl, c);
+  uint32_t c2 = 0;
+  hi = addc(hi, ph, c2);
+  uint32_t c3 = 0;
+  hi = addc(hi, (uint64_t)c, c3);
+  top += c2 + c3;
+}
+
+template <int JB>
+__global__ __launch_bounds__(256) void mac_kernel(MacArgs a, int j0) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per_col = (long long)a.nl * a.d;
+  if (gid >= a.ncols * per_col) return;
+  const long long col = gid / per_col;
+  const int lk = (int)(gid % per_col);  // limb * d + coeff
+  const int l = lk / a.d;
+  const int J = min(JB, a.J - j0);
+  uint64_t lo[JB], hi[JB];
+  uint32_t top[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) lo[j] = hi[j] = top[j] = 0;
+  const uint64_t* b1 = a.B1 + col * a.b1_col + lk;
+  for (int t = 0; t < a.T1; ++t) {
+    const uint64_t x = b1[t * a.b1_term];
+#pragma unroll
+    for (int j = 0; j < JB; ++j)
+      if (j < J) acc_add(lo[j], hi[j], top[j], a.A1[((long long)(j0 + j) * a.T1 + t) * per_col + lk], x);
+  }
+  if (a.T2) {
+    const uint64_t* b2 = a.B2 + col * a.b2_col + lk;
+    for (int t = 0; t < a.T2; ++t) {
+      const uint64_t x = b2[t * a.b2_term];
+#pragma unroll
+      for (int j = 0; j < JB; ++j)
+        if (j < J) acc_add(lo[j], hi[j], top[j], a.A2[((long long)(j0 + j) * a.T2 + t) * per_col + lk], x);
+    }
+  }
+  const RnsPrime& P = a.P[l];
+  const uint64_t q = P.q;
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    if (j >= J) continue;
+    // (lo + hi 2^64 + top 2^128) * 2^-64 = lo 2^-64 + hi + top 2^64  (mod q)
+    uint64_t r = sh_mul(lo[j], P.rinv, P.rinv_sh, q);
+    r = mod_add(r, sh_mul(hi[j], 1, P.one_sh, q), q);
+    r = mod_add(r, sh_mul((uint64_t)top[j], P.r64, P.r64_sh, q), q);
+    if (a.C) r = mod_add(a.C[col * a.c_col + (long long)(j0 + j) * a.c_j + lk], r, q);
+    a.out[(col * a.J + j0 + j) * per_col + lk] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. round: IMForm -> INTT -> centred CRT -> floor shift -> mod q' -> MForm -> NTT
+// ------------------------------------------------------------------------------------------
+struct RoundArgs {
+  int d, cut;
+  RingDev src, dst;
+  CrtDev crt;
+  DstDev dm;
+  const uint64_t* in;  // [npoly][src.n][d]
+  uint64_t* out;       // [npoly] at stride out_stride, dst.n limbs (+ zero rows up to out_rows)
+  long long out_stride;
+  int out_rows;
+};
+
+__device__ __forceinline__ void mw_muladd(uint64_t* v, int nw, uint64_t m, uint64_t add) {
+  uint64_t carry = add;
+  for (int i = 0; i < nw; ++i) {
+    uint64_t lo, hi;
+    mul_wide(v[i], m, lo, hi);
+    uint32_t c = 0;
+    lo = addc(lo, carry, c);
+    v[i] = lo;
+    carry = hi + c;
+  }
+}
+
+__global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
+  __shared__ uint64_t poly[kMaxQ][kMaxD];
+  const int d = a.d, tid = threadIdx.x, ns = a.src.n, nd = a.dst.n;
+  const long long pid = blockIdx.x;
+  const uint64_t* in = a.in + pid * ns * d;
+  for (int k = tid; k < ns * d; k += blockDim.x) {
+    const int l = k / d;
+    const RnsPrime& P = a.src.p[l];
+    poly[l][k % d] = sh_mul(in[k], P.rinv, P.rinv_sh, P.q);  // IMForm
+  }
+  __syncthreads();
+  const int half = blockDim.x >> 1;
+  for (int l0 = 0; l0 < ns; l0 += 2) {
+    const int l = l0 + (tid >= half ? 1 : 0);
+    const bool active = l < ns;
+    const int lc = active ? l : l0;
+    intt_lds(poly[lc], d, a.src.bwd + (long long)lc * d, a.src.p[lc], tid % half, half, active);
+  }
+  // CRT per coefficient
+  for (int k = tid; k < d; k += blockDim.x) {
+    uint64_t r[kMaxQ];
+    for (int l = 0; l < ns; ++l) r[l] = poly[l][k];
+    bool neg;
+    uint64_t mag[4] = {0, 0, 0, 0};
+    if (ns == 1) {  // reconstructTo fast path: toBalanced (rns.go:68-73,78-91)
+      const uint64_t q = a.crt.q[0];
+      neg = r[0] > (q >> 1);
+      mag[0] = neg ? q - r[0] : r[0];
+    } else {  // Garner: V = x0 + q0 (x1 + q1 (x2 + ...)) in [0, Q)  (rns.go:93-99)
+      uint64_t x[kMaxQ];
+      for (int j = 0; j < ns; ++j) {
+        const uint64_t qj = a.crt.q[j];
+        uint64_t v = r[j];
+        for (int kk = 0; kk < j; ++kk) {
+          const uint64_t xk = x[kk] >= qj ? x[kk] % qj : x[kk];
+          v = mod_sub(v, xk, qj);
+          v = sh_mul(v, a.crt.inv[j][kk], a.crt.inv_sh[j][kk], qj);
+        }
+        x[j] = v;
+      }
+      uint64_t V[4] = {x[ns - 1], 0, 0, 0};
+      for (int j = ns - 2; j >= 0; --j) mw_muladd(V, 4, a.crt.q[j], x[j]);
+      // V >= floor(Q/2) -> V - Q (rns.go:100-102)
+      bool ge = true;
+      for (int i = 3; i >= 0; --i) {
+        if (V[i] != a.crt.Qhalf[i]) {
+          ge = V[i] > a.crt.Qhalf[i];
+          break;
+        }
+      }
+      neg = ge;
+      if (neg) {
+        uint32_t br = 0;
+        for (int i = 0; i < 4; ++i) mag[i] = subb(a.crt.Q[i], V[i], br);
+      } else {
+        for (int i = 0; i < 4; ++i) mag[i] = V[i];
+      }
+    }
+    // floor(value / 2^cut) (big.Int.Rsh on a signed value rounds toward -inf)
+    bool lost = false;
+    int cut = a.cut;
+    while (cut > 0) {
+      const int sft = cut > 63 ? 63 : cut;
+      lost |= (mag[0] & ((1ull << sft) - 1)) != 0;
+      for (int i = 0; i < 4; ++i) mag[i] = (mag[i] >> sft) | (i + 1 < 4 ? mag[i + 1] << (64 - sft) : 0);
+      cut -= sft;
+    }
+    if (neg && lost) {
+      for (int i = 0; i < 4; ++i)
+        if (++mag[i]) break;
+    }
+    const bool zero = !(mag[0] | mag[1] | mag[2] | mag[3]);
+    // setBigCoeffTo: Euclidean mod each destination prime (rns.go:108-114), then MForm
+    for (int l = 0; l < nd; ++l) {
+      const RnsPrime& P = a.dst.p[l];
+      const uint64_t q = P.q;
+      uint64_t m = 0;
+      for (int i = 0; i < 4; ++i) m = mod_add(m, sh_mul(mag[i], a.dm.pw[l][i], a.dm.pw_sh[l][i], q), q);
+      if (neg && !zero) m = mod_neg(m, q);
+      r[l] = sh_mul(m, P.r64, P.r64_sh, q);
+    }
+    for (int l = 0; l < nd; ++l) poly[l][k] = r[l];  // each thread owns coefficient k
+  }
+  __syncthreads();
+  for (int l0 = 0; l0 < nd; l0 += 2) {
+    const int l = l0 + (tid >= half ? 1 : 0);
+    const bool active = l < nd;
+    const int lc = active ? l : l0;
+    ntt_lds(poly[lc], d, a.dst.fwd + (long long)lc * d, a.dst.p[lc].q, tid % half, half, active);
+  }
+  uint64_t* out = a.out + pid * a.out_stride;
+  for (int k = tid; k < a.out_rows * d; k += blockDim.x) out[k] = (k / d < nd) ? poly[k / d][k % d] : 0;
+}
+
+}  // namespace rg
+
+// ------------------------------------------------------------------------------------------
+// host
+// ------------------------------------------------------------------------------------------
+struct rg_jindo {
+  rg_jindo_params p;
+  rg_field field;
+  rg::RnsPrime rq[rg::kMaxQ], ro[rg::kMaxQ];
+  rg::DevBuf rootsq_f, rootsq_b, rootso_f, rootso_b;
+  rg::CrtDev crt_q, crt_o;
+  rg::DstDev dst_o;
+  std::vector<uint64_t> h_ck_in, h_ck_mlwe, h_ck_out;
+  rg::DevBuf ck_in, ck_mlwe, ck_out;
+  uint64_t base_inv;
+  std::mutex mu;  // guards the scratch cache
+  rg::DevBuf s_digits, s_com, s_ocom, s_skip;
+  size_t scratch_batch = 0;
+};
+
+namespace rg {
+
+// ring.PrimitiveRoot: smallest g >= 3 that generates Z_q^* (factors by trial division +
+// Pollard rho; q < 2^62)
+static bool is_prime_u64(uint64_t n) {
+  if (n < 2) return false;
+  static const uint64_t sp[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  for (uint64_t p : sp)
+    if (n % p == 0) return n == p;
+  uint64_t d = n - 1;
+  int r = 0;
+  while (!(d & 1)) d >>= 1, ++r;
+  for (uint64_t a : sp) {
+    uint64_t x = h_powmod(a, d, n);
+    if (x == 1 || x == n - 1) continue;
+    bool ok = false;
+    for (int k = 1; k < r && !ok; ++k) {
+      x = h_mulmod(x, x, n);
+      ok = x == n - 1;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+static uint64_t gcd_u64(uint64_t a, uint64_t b) {
+  while (b) {
+    uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+static uint64_t rho(uint64_t n) {
+  if (!(n & 1)) return 2;
+  for (uint64_t c = 1;; ++c) {
+    uint64_t x = 2, y = 2, g = 1;
+    while (g == 1) {
+      x = (h_mulmod(x, x, n) + c) % n;
+      y = (h_mulmod(y, y, n) + c) % n;
+      y = (h_mulmod(y, y, n) + c) % n;
+      g = gcd_u64(x > y ? x - y : y - x, n);
+    }
+    if (g != n) return g;
+  }
+}
+static void factor(uint64_t n, std::vector<uint64_t>& f) {
+  if (n == 1) return;
+  if (is_prime_u64(n)) {
+    if (std::find(f.begin(), f.end(), n) == f.end()) f.push_back(n);
+    return;
+  }
+  uint64_t dv = rho(n);
+  factor(dv, f);
+  factor(n / dv, f);
+}
+static uint64_t primitive_root(uint64_t q) {
+  std::vector<uint64_t> f;
+  factor(q - 1, f);
+  for (uint64_t g = 3;; ++g) {
+    bool ok = true;
+    for (uint64_t p : f) ok = ok && h_powmod(g, (q - 1) / p, q) != 1;
+    if (ok) return g;
+  }
+}
+static uint64_t brv(uint64_t x, int logn) {
+  uint64_t r = 0;
+  for (int i = 0; i < logn; ++i) r = (r << 1) | ((x >> i) & 1);
+  return r;
+}
+
+static rg_status make_ring(int d, const uint64_t* primes, int n, uint64_t base, RnsPrime* P, DevBuf& fwd, DevBuf& bwd) {
+  int logd = 0;
+  while ((1 << logd) < d) ++logd;
+  std::vector<ulonglong2> f((size_t)n * d), b((size_t)n * d);
+  for (int l = 0; l < n; ++l) {
+    const uint64_t q = primes[l];
+    if (!is_prime_u64(q) || (q - 1) % (2 * (uint64_t)d) || (q >> 62)) return RG_ERR_INVALID;
+    RnsPrime& R = P[l];
+    R.q = q;
+    R.r64 = (uint64_t)(((unsigned __int128)1 << 64) % q);
+    R.r64_sh = h_shoup(R.r64, q);
+    R.rinv = h_powmod(R.r64, q - 2, q);
+    R.rinv_sh = h_shoup(R.rinv, q);
+    R.one_sh = h_shoup(1, q);
+    R.ninv = h_powmod((uint64_t)d, q - 2, q);
+    R.ninv_sh = h_shoup(R.ninv, q);
+    R.bmod = base % q;
+    R.bmod_sh = h_shoup(R.bmod, q);
+    const uint64_t g = primitive_root(q);
+    const uint64_t psi = h_powmod(g, (q - 1) / (2 * (uint64_t)d), q), psii = h_powmod(psi, q - 2, q);
+    uint64_t x = 1, y = 1;
+    for (int j = 0; j < d; ++j) {
+      const size_t k = (size_t)l * d + brv((uint64_t)j, logd);
+      f[k].x = x;
+      f[k].y = h_shoup(x, q);
+      b[k].x = y;
+      b[k].y = h_shoup(y, q);
+      x = h_mulmod(x, psi, q);
+      y = h_mulmod(y, psii, q);
+    }
+  }
+  RG_TRY(fwd.upload(f.data(), f.size() * sizeof(ulonglong2)));
+  RG_TRY(bwd.upload(b.data(), b.size() * sizeof(ulonglong2)));
+  return RG_OK;
+}
+
+static void make_crt(const uint64_t* primes, int n, CrtDev& C) {
+  memset(&C, 0, sizeof(C));
+  C.n = n;
+  for (int j = 0; j < n; ++j) {
+    C.q[j] = primes[j];
+    for (int k = 0; k < j; ++k) {
+      C.inv[j][k] = h_powmod(primes[k] % primes[j], primes[j] - 2, primes[j]);
+      C.inv_sh[j][k] = h_shoup(C.inv[j][k], primes[j]);
+    }
+  }
+  unsigned __int128 acc;
+  uint64_t Q[5] = {1, 0, 0, 0, 0};
+  for (int j = 0; j < n; ++j) {
+    uint64_t carry = 0;
+    for (int i = 0; i < 4; ++i) {
+      acc = (unsigned __int128)Q[i] * primes[j] + carry;
+      Q[i] = (uint64_t)acc;
+      carry = (uint64_t)(acc >> 64);
+    }
+  }
+  for (int i = 0; i < 4; ++i) {
+    C.Q[i] = Q[i];
+    C.Qhalf[i] = (Q[i] >> 1) | (i + 1 < 4 ? Q[i + 1] << 63 : 0);
+  }
+}
+
+static void make_dst(const uint64_t* primes, int n, DstDev& D) {
+  memset(&D, 0, sizeof(D));
+  D.n = n;
+  for (int l = 0; l < n; ++l) {
+    const uint64_t q = primes[l];
+    uint64_t p = 1 % q;
+    const uint64_t r64 = (uint64_t)(((unsigned __int128)1 << 64) % q);
+    for (int i = 0; i < 4; ++i) {
+      D.pw[l][i] = p;
+      D.pw_sh[l][i] = h_shoup(p, q);
+      p = h_mulmod(p, r64, q);
+    }
+  }
+}
+
+static RingDev ring_dev(const RnsPrime* P, int n, const DevBuf& f, const DevBuf& b) {
+  RingDev R;
+  memset(&R, 0, sizeof(R));
+  R.n = n;
+  for (int l = 0; l < n; ++l) R.p[l] = P[l];
+  R.fwd = f.as<const ulonglong2>();
+  R.bwd = b.as<const ulonglong2>();
+  return R;
+}
+
+static JShape shape_of(const rg_jindo_params& p, long long nv) {
+  JShape s;
+  s.rank = p.rank;
+  s.rows = p.rows;
+  s.cols = p.cols;
+  s.slots = p.slots;
+  s.exp = p.exp;
+  s.d = p.d;
+  s.in_msis = p.in_msis;
+  s.out_msis = p.out_msis;
+  s.mlwe = p.mlwe;
+  s.dcmp = p.dcmp;
+  s.log_in_cut = p.log_in_cut;
+  s.log_out_cut = p.log_out_cut;
+  s.nq = p.nq;
+  s.nqo = p.nqo;
+  s.base = p.base;
+  s.nv = nv;
+  return s;
+}
+
+static rg_status validate(const rg_jindo_params* p) {
+  if (!p) return RG_ERR_INVALID;
+  if (p->nq < 1 || p->nq > kMaxQ || p->nqo < 1 || p->nqo > kMaxQ || p->nqo > p->nq) return RG_ERR_INVALID;
+  if (p->d < 2 || p->d > kMaxD || (p->d & (p->d - 1))) return RG_ERR_INVALID;
+  if (p->rows < 2 || p->cols < 1 || p->slots < 1 || p->exp < 1 || p->slots * p->exp > p->d) return RG_ERR_INVALID;
+  if (p->in_msis < 1 || p->in_msis > kMaxJ || p->out_msis < 1 || p->out_msis > kMaxJ || p->mlwe < 0) return RG_ERR_INVALID;
+  if (p->dcmp != (p->cols + 1) * p->in_msis) return RG_ERR_INVALID;
+  if (p->base < 2 || (p->base >> 32)) return RG_ERR_INVALID;
+  if (!(p->field_limbs == 1 || p->field_limbs == 2 || p->field_limbs == 4 || p->field_limbs == 7 ||
+        p->field_limbs == 14))
+    return RG_ERR_UNSUPPORTED;
+  return RG_OK;
+}
+
+static rg_status build(rg_jindo* J) {
+  const rg_jindo_params& p = J->p;
+  if (!init_field(&J->field, p.field_limbs, p.field_q)) return RG_ERR_INVALID;
+  RG_TRY(make_ring(p.d, p.q, p.nq, p.base, J->rq, J->rootsq_f, J->rootsq_b));
+  RG_TRY(make_ring(p.d, p.qo, p.nqo, p.base, J->ro, J->rootso_f, J->rootso_b));
+  make_crt(p.q, p.nq, J->crt_q);
+  make_crt(p.qo, p.nqo, J->crt_o);
+  make_dst(p.qo, p.nqo, J->dst_o);
+  J->base_inv = (uint64_t)(((unsigned __int128)1 << 64) / p.base);
+  return RG_OK;
+}
+
+static size_t ck_sizes(const rg_jindo_params& p, size_t* in, size_t* ml, size_t* out) {
+  *in = (size_t)p.in_msis * p.rows * p.nq * p.d;
+  *ml = (size_t)p.in_msis * p.mlwe * p.nq * p.d;
+  *out = (size_t)p.out_msis * p.dcmp * p.nqo * p.d;
+  return *in + *ml + *out;
+}
+
+template <int L>
+static rg_status launch_digits(const rg_jindo* J, size_t batch, const uint64_t* v, long long nv, const uint64_t* last,
+                               const uint64_t* mask, uint32_t* digits, hipStream_t st) {
+  DigitArgs<L> a;
+  a.s = shape_of(J->p, nv);
+  memcpy(a.F.q, J->field.q, 8 * L);
+  a.F.qinv = J->field.qinv;
+  a.base_inv = J->base_inv;
+  a.v = v;
+  a.last_row = last;
+  a.mask = mask;
+  a.digits = digits;
+  a.total = (long long)batch * (J->p.cols + 1) * J->p.rows * J->p.slots;
+  const long long blocks = (a.total + 255) / 256;
+  hipLaunchKernelGGL(digits_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return check_launch("jindo digits");
+}
+
+static rg_status ensure_scratch(rg_jindo* J, size_t batch) {
+  const rg_jindo_params& p = J->p;
+  const size_t d = p.d;
+  const size_t encs = batch * (p.cols + 1) * p.rows;
+  RG_TRY(J->s_digits.alloc(encs * d * 4));
+  RG_TRY(J->s_com.alloc(batch * (p.cols + 1) * p.in_msis * p.nq * d * 8));
+  RG_TRY(J->s_ocom.alloc(batch * p.out_msis * p.nqo * d * 8));
+  return RG_OK;
+}
+
+static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
+                            const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
+                            uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  if (nv < 1 || nv > (size_t)p.rank) return RG_ERR_RANK;
+  if (batch == 0) return RG_OK;
+  std::lock_guard<std::mutex> lk(J->mu);
+  RG_TRY(ensure_scratch(J, batch));
+  const int d = p.d, nq = p.nq, nqo = p.nqo, nm = p.in_msis + p.mlwe;
+  const long long cs = (long long)p.cols * p.slots;
+  // encodes the reference skips (prover.go:101-105, 118-123) -- same for every commit
+  std::vector<uint8_t> skip((size_t)(p.cols + 1) * p.rows, 0);
+  for (int i = 0; i <= p.cols; ++i)
+    for (int j = 1; j < p.rows - 1; ++j) {
+      const long long start = (i == p.cols) ? j * cs : j * cs + (long long)i * p.slots;
+      if (start > (long long)nv)
+        for (int jj = j; jj < p.rows - 1; ++jj) skip[(size_t)i * p.rows + jj] = 1;
+      if (start > (long long)nv) break;
+    }
+  RG_TRY(J->s_skip.alloc(skip.size()));
+  RG_HIP(hipMemcpyAsync(J->s_skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, st));
+  RG_HIP(hipStreamSynchronize(st));  // `skip` is a stack vector
+
+  // 1. digits
+  uint32_t* digits = J->s_digits.as<uint32_t>();
+  rg_status s;
+  switch (p.field_limbs) {
+    case 1: s = launch_digits<1>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+    case 2: s = launch_digits<2>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+    case 4: s = launch_digits<4>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+    case 7: s = launch_digits<7>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+    default: s = launch_digits<14>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+  }
+  RG_TRY(s);
+  // 2. prep (encodes + MLWE polys)
+  PrepArgs pa;
+  pa.s = shape_of(p, (long long)nv);
+  pa.R = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
+  pa.digits = digits;
+  pa.enc_noise = reinterpret_cast<const long long*>(d_en);
+  pa.mlwe_noise = reinterpret_cast<const long long*>(d_mn);
+  pa.skip = J->s_skip.as<uint8_t>();
+  pa.enc = d_enc;
+  pa.mlwe = d_mlwe;
+  pa.n_enc = (long long)batch * (p.cols + 1) * p.rows;
+  const long long n_ml = (long long)batch * (p.cols + 1) * nm;
+  hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
+  RG_TRY(check_launch("jindo prep"));
+  // 3. inner MAC
+  MacArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.d = d;
+  ma.nl = nq;
+  ma.J = p.in_msis;
+  ma.ncols = (long long)batch * (p.cols + 1);
+  ma.T1 = p.rows;
+  ma.A1 = J->ck_in.as<uint64_t>();
+  ma.B1 = d_enc;
+  ma.b1_col = (long long)p.rows * nq * d;
+  ma.b1_term = (long long)nq * d;
+  ma.T2 = p.mlwe;
+  ma.A2 = J->ck_mlwe.as<uint64_t>();
+  ma.B2 = d_mlwe;
+  ma.b2_col = (long long)nm * nq * d;
+  ma.b2_term = (long long)nq * d;
+  ma.C = d_mlwe + (long long)p.mlwe * nq * d;  // MLWE[i][mlwe + j]
+  ma.c_col = (long long)nm * nq * d;
+  ma.c_j = (long long)nq * d;
+  ma.out = J->s_com.as<uint64_t>();
+  for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
+  {
+    const long long threads = ma.ncols * nq * d;
+    for (int j0 = 0; j0 < ma.J; j0 += 8) {
+      hipLaunchKernelGGL(mac_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ma, j0);
+      RG_TRY(check_launch("jindo mac"));
+    }
+  }
+  // 4. inner round -> Opening.InCommit (column i, j -> index i*inMSIS + j)
+  RoundArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  ra.d = d;
+  ra.cut = p.log_in_cut;
+  ra.src = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
+  ra.dst = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
+  ra.crt = J->crt_q;
+  ra.dm = J->dst_o;
+  ra.in = J->s_com.as<uint64_t>();
+  ra.out = d_incom;
+  ra.out_stride = (long long)nqo * d;
+  ra.out_rows = nqo;
+  {
+    const long long npoly = (long long)batch * (p.cols + 1) * p.in_msis;  // == batch * dcmp, same order
+    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), 0, st, ra);
+    RG_TRY(check_launch("jindo round(in)"));
+  }
+  // 5. outer MAC + round -> Commitment.Value (ringQ-shaped rows, rows >= nqo zero)
+  MacArgs mo;
+  memset(&mo, 0, sizeof(mo));
+  mo.d = d;
+  mo.nl = nqo;
+  mo.J = p.out_msis;
+  mo.ncols = (long long)batch;
+  mo.T1 = p.dcmp;
+  mo.A1 = J->ck_out.as<uint64_t>();
+  mo.B1 = d_incom;
+  mo.b1_col = (long long)p.dcmp * nqo * d;
+  mo.b1_term = (long long)nqo * d;
+  mo.out = J->s_ocom.as<uint64_t>();
+  for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
+  {
+    const long long threads = mo.ncols * nqo * d;
+    for (int j0 = 0; j0 < mo.J; j0 += 8) {
+      hipLaunchKernelGGL(mac_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, mo, j0);
+      RG_TRY(check_launch("jindo mac(out)"));
+    }
+  }
+  RoundArgs ro = ra;
+  ro.cut = p.log_out_cut;
+  ro.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
+  ro.crt = J->crt_o;
+  ro.in = J->s_ocom.as<uint64_t>();
+  ro.out = d_com;
+  ro.out_stride = (long long)nq * d;
+  ro.out_rows = nq;
+  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), 0, st, ro);
+  RG_TRY(check_launch("jindo round(out)"));
+  return RG_OK;
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+extern "C" {
+
+static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** J) {
+  if (!out) return RG_ERR_INVALID;
+  *out = nullptr;
+  RG_TRY(validate(p));
+  *J = new rg_jindo();
+  (*J)->p = *p;
+  rg_status s = build(*J);
+  if (s != RG_OK) {
+    delete *J;
+    *J = nullptr;
+  }
+  return s;
+}
+
+static rg_status upload_ck(rg_jindo* J) {
+  RG_TRY(J->ck_in.upload(J->h_ck_in.data(), J->h_ck_in.size() * 8));
+  if (!J->h_ck_mlwe.empty()) RG_TRY(J->ck_mlwe.upload(J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8));
+  RG_TRY(J->ck_out.upload(J->h_ck_out.data(), J->h_ck_out.size() * 8));
+  return RG_OK;
+}
+
+rg_status rg_jindo_create(const rg_jindo_params* p, const uint64_t* ck_in, const uint64_t* ck_mlwe,
+                          const uint64_t* ck_out, rg_jindo** out) {
+  if (!ck_in || !ck_out || (!ck_mlwe && p && p->mlwe)) return RG_ERR_INVALID;
+  rg_jindo* J = nullptr;
+  RG_TRY(jindo_new(p, out, &J));
+  size_t a, b, c;
+  ck_sizes(J->p, &a, &b, &c);
+  J->h_ck_in.assign(ck_in, ck_in + a);
+  if (b) J->h_ck_mlwe.assign(ck_mlwe, ck_mlwe + b);
+  J->h_ck_out.assign(ck_out, ck_out + c);
+  rg_status s = upload_ck(J);
+  if (s != RG_OK) {
+    delete J;
+    return s;
+  }
+  *out = J;
+  return RG_OK;
+}
+
+rg_status rg_jindo_create_from_crs(const rg_jindo_params* p, const uint8_t* crs, size_t crs_len, rg_jindo** out) {
+  if (!crs && crs_len) return RG_ERR_INVALID;
+  rg_jindo* J = nullptr;
+  RG_TRY(jindo_new(p, out, &J));
+  const rg_jindo_params& P = J->p;
+  CtrStream u(crs, crs_len);
+  if (!u.ok) {
+    delete J;
+    set_last_error("libcrypto (SHA384/AES-256-CTR) unavailable");
+    return RG_ERR_UNSUPPORTED;
+  }
+  size_t a, b, c;
+  ck_sizes(P, &a, &b, &c);
+  J->h_ck_in.assign(a, 0);
+  J->h_ck_mlwe.assign(b, 0);
+  J->h_ck_out.assign(c, 0);
+  const size_t d = P.d;
+  // entities.go:24-61: In, then MLWE, then Out; coefficient-major, limb-minor draws
+  for (int i = 0; i < P.in_msis; ++i)
+    for (int j = 0; j < P.rows; ++j)
+      for (size_t k = 0; k < d; ++k)
+        for (int l = 0; l < P.nq; ++l) J->h_ck_in[(((size_t)i * P.rows + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
+  for (int i = 0; i < P.in_msis; ++i)
+    for (int j = 0; j < P.mlwe; ++j)
+      for (size_t k = 0; k < d; ++k)
+        for (int l = 0; l < P.nq; ++l) J->h_ck_mlwe[(((size_t)i * P.mlwe + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
+  for (int i = 0; i < P.out_msis; ++i)
+    for (int j = 0; j < P.dcmp; ++j)
+      for (size_t k = 0; k < d; ++k)
+        for (int l = 0; l < P.nqo; ++l) J->h_ck_out[(((size_t)i * P.dcmp + j) * P.nqo + l) * d + k] = u.sample_n(P.qo[l]);
+  rg_status s = upload_ck(J);
+  if (s != RG_OK) {
+    delete J;
+    return s;
+  }
+  *out = J;
+  return RG_OK;
+}
+
+void rg_jindo_destroy(rg_jindo* j) { delete j; }
+
+rg_status rg_jindo_commit_key(const rg_jindo* J, uint64_t* ck_in, uint64_t* ck_mlwe, uint64_t* ck_out) {
+  if (!J) return RG_ERR_INVALID;
+  if (ck_in) memcpy(ck_in, J->h_ck_in.data(), J->h_ck_in.size() * 8);
+  if (ck_mlwe && !J->h_ck_mlwe.empty()) memcpy(ck_mlwe, J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8);
+  if (ck_out) memcpy(ck_out, J->h_ck_out.data(), J->h_ck_out.size() * 8);
+  return RG_OK;
+}
+
+size_t rg_jindo_scratch_bytes(const rg_jindo* J, size_t batch) {
+  if (!J) return 0;
+  const rg_jindo_params& p = J->p;
+  const size_t d = p.d;
+  return batch * (p.cols + 1) * p.rows * d * 4 + batch * (p.cols + 1) * p.in_msis * p.nq * d * 8 +
+         batch * p.out_msis * p.nqo * d * 8 + (size_t)(p.cols + 1) * p.rows;
+}
+
+rg_status rg_jindo_commit_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
+                              const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
+                              uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream) {
+  if (!J) return RG_ERR_INVALID;
+  if (batch && (!d_v || !d_last || !d_mask || !d_en || !d_mn || !d_incom || !d_enc || !d_mlwe || !d_com))
+    return RG_ERR_INVALID;
+  return commit_dev(const_cast<rg_jindo*>(J), batch, d_v, nv, d_last, d_mask, d_en, d_mn, d_incom, d_enc, d_mlwe, d_com,
+                    as_stream(stream));
+}
+
+rg_status rg_jindo_commit(const rg_jindo* J, const uint64_t* v, size_t nv, const uint64_t* last_row,
+                          const uint64_t* mask, const int64_t* enc_noise, const int64_t* mlwe_noise, uint64_t* o_incom,
+                          uint64_t* o_enc, uint64_t* o_mlwe, uint64_t* o_com) {
+  if (!J || !v || !last_row || !mask || !enc_noise || !mlwe_noise || !o_incom || !o_enc || !o_mlwe || !o_com)
+    return RG_ERR_INVALID;
+  const rg_jindo_params& p = J->p;
+  if (nv < 1 || nv > (size_t)p.rank) return RG_ERR_RANK;
+  const size_t L = p.field_limbs, d = p.d, nm = p.in_msis + p.mlwe;
+  const size_t b_v = nv * L * 8, b_last = (size_t)p.cols * p.slots * L * 8, b_mask = (size_t)p.rows * p.slots * L * 8;
+  const size_t b_en = (size_t)(p.cols + 1) * p.rows * d * 8, b_mn = (size_t)(p.cols + 1) * nm * d * 8;
+  const size_t b_inc = (size_t)p.dcmp * p.nqo * d * 8, b_enc = (size_t)(p.cols + 1) * p.rows * p.nq * d * 8;
+  const size_t b_ml = (size_t)(p.cols + 1) * nm * p.nq * d * 8, b_com = (size_t)p.out_msis * p.nq * d * 8;
+  DevBuf v_, l_, m_, en_, mn_, inc_, enc_, ml_, com_;
+  RG_TRY(v_.upload(v, b_v));
+  RG_TRY(l_.upload(last_row, b_last));
+  RG_TRY(m_.upload(mask, b_mask));
+  RG_TRY(en_.upload(enc_noise, b_en));
+  RG_TRY(mn_.upload(mlwe_noise, b_mn));
+  RG_TRY(inc_.alloc(b_inc));
+  RG_TRY(enc_.alloc(b_enc));
+  RG_TRY(ml_.alloc(b_ml));
+  RG_TRY(com_.alloc(b_com));
+  RG_TRY(rg_jindo_commit_dev(J, 1, v_.as<uint64_t>(), nv, l_.as<uint64_t>(), m_.as<uint64_t>(), en_.as<int64_t>(),
+                             mn_.as<int64_t>(), inc_.as<uint64_t>(), enc_.as<uint64_t>(), ml_.as<uint64_t>(),
+                             com_.as<uint64_t>(), nullptr));
+  RG_HIP(hipMemcpy(o_incom, inc_.p, b_inc, hipMemcpyDeviceToHost));
+  RG_HIP(hipMemcpy(o_enc, enc_.p, b_enc, hipMemcpyDeviceToHost));
+  RG_HIP(hipMemcpy(o_mlwe, ml_.p, b_ml, hipMemcpyDeviceToHost));
+  RG_HIP(hipMemcpy(o_com, com_.p, b_com, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+
+}  // extern "C"

@@ -82,6 +82,14 @@ def header_symbols():
 def lib():
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch-ROCm bundles its own libamdhip64 (SONAME
+        # libamdhip64.so.7).  Loading torch first makes libringo's NEEDED entry resolve to
+        # that same copy, so device pointers and streams are shared; loading libringo first
+        # would start /opt/rocm's runtime and torch would then fail to see any GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libringo.so not built at {LIB_PATH}: run __graft_entry__.build() "
                                "(there is no CPU fallback for the product path)")

@@ -1,1 +1,160 @@
-"""jindo mirror (jindo/) over libringo -- filled in with the Jindo commit pipeline."""
+"""jindo mirror (jindo/) over libringo.
+
+    params = Parameters(...)            # shapes as jindo.Parameters holds them (params.go:64-123)
+    prv = NewProver(params, b"Jindo!")  # prover.go:28 (commit key derived from the CRS on the host)
+    com, open_ = prv.Commit(v, rnd)     # prover.go:45, randomness injected (see Randomness)
+
+The reference's Commit draws its randomness internally (crypto/rand, Gaussian samplers); this
+mirror takes those draws as arguments so the result is bit-exact against Go given identical
+draws.  The Go-side NewParameters float search is not re-derived here: shapes
+are passed in (tests take them from committed fixtures).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import JindoParamsC, check, iptr, lib, ptr, vp
+from .bigpoly import RingoPanic, _addr, _stream
+
+
+@dataclass
+class Parameters:
+    rank: int
+    rows: int
+    cols: int
+    slots: int
+    exp: int
+    d: int
+    in_msis: int
+    out_msis: int
+    mlwe: int
+    dcmp: int
+    log_in_cut: int
+    log_out_cut: int
+    base: int
+    q: list
+    qo: list
+    field_q: int
+
+    @classmethod
+    def from_dict(cls, P, field_q):
+        return cls(rank=P["rank"], rows=P["rows"], cols=P["cols"], slots=P["slots"], exp=P["exp"], d=P["d"],
+                   in_msis=P["in_msis"], out_msis=P["out_msis"], mlwe=P["mlwe"], dcmp=P["in_com_dcmp_len"],
+                   log_in_cut=P["log_in_cut"], log_out_cut=P["log_out_cut"], base=P["base"], q=list(P["q"]),
+                   qo=list(P["qo"]), field_q=int(field_q))
+
+    @property
+    def L(self):
+        return (self.field_q.bit_length() + 63) // 64
+
+    @property
+    def nq(self):
+        return len(self.q)
+
+    @property
+    def nqo(self):
+        return len(self.qo)
+
+    def c_struct(self):
+        s = JindoParamsC()
+        for k in ["rank", "rows", "cols", "slots", "exp", "d", "in_msis", "out_msis", "mlwe", "dcmp", "log_in_cut",
+                  "log_out_cut"]:
+            setattr(s, k, int(getattr(self, k)))
+        s.base = self.base
+        s.nq, s.nqo = self.nq, self.nqo
+        for i, x in enumerate(self.q):
+            s.q[i] = x
+        for i, x in enumerate(self.qo):
+            s.qo[i] = x
+        s.field_limbs = self.L
+        for i in range(self.L):
+            s.field_q[i] = (self.field_q >> (64 * i)) & ((1 << 64) - 1)
+        return s
+
+    # array shapes (include/ringo.h rg_jindo_commit)
+    def shapes(self, batch=None):
+        nm = self.in_msis + self.mlwe
+        sh = dict(last_row=(self.cols * self.slots, self.L), mask=(self.rows, self.slots, self.L),
+                  enc_noise=(self.cols + 1, self.rows, self.d), mlwe_noise=(self.cols + 1, nm, self.d),
+                  incom=(self.dcmp, self.nqo, self.d), enc=(self.cols + 1, self.rows, self.nq, self.d),
+                  mlwe_out=(self.cols + 1, nm, self.nq, self.d), com=(self.out_msis, self.nq, self.d))
+        if batch is not None:
+            sh = {k: (batch,) + v for k, v in sh.items()}
+        return sh
+
+    def ck_shapes(self):
+        return dict(ck_in=(self.in_msis, self.rows, self.nq, self.d),
+                    ck_mlwe=(self.in_msis, self.mlwe, self.nq, self.d),
+                    ck_out=(self.out_msis, self.dcmp, self.nqo, self.d))
+
+
+@dataclass
+class Randomness:
+    """The draws Prover.Commit makes internally (prover.go:65-139), injected."""
+    last_row: np.ndarray    # [cols*slots][L] Montgomery, last entry 0
+    mask: np.ndarray        # [rows][slots][L]
+    enc_noise: np.ndarray   # [cols+1][rows][d] int64
+    mlwe_noise: np.ndarray  # [cols+1][inMSIS+mlwe][d] int64
+
+
+@dataclass
+class Opening:  # entities.go:103-107
+    InCommit: np.ndarray
+    Encode: np.ndarray
+    MLWE: np.ndarray
+
+
+@dataclass
+class Commitment:  # entities.go:80-82
+    Value: np.ndarray
+
+
+class Prover:
+    def __init__(self, params, crs=None, ck=None):
+        self.params = params
+        h = vp()
+        ps = params.c_struct()
+        if ck is not None:
+            a, b, c = (np.ascontiguousarray(x, np.uint64) for x in ck)
+            st = lib().rg_jindo_create(ctypes.byref(ps), ptr(a), ptr(b), ptr(c), ctypes.byref(h))
+        else:
+            st = lib().rg_jindo_create_from_crs(ctypes.byref(ps), crs, len(crs), ctypes.byref(h))
+        check(st)
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rg_jindo_destroy(self.h)
+            self.h = None
+
+    def commit_key(self):
+        sh = self.params.ck_shapes()
+        out = {k: np.zeros(v, np.uint64) for k, v in sh.items()}
+        check(lib().rg_jindo_commit_key(self.h, ptr(out["ck_in"]), ptr(out["ck_mlwe"]), ptr(out["ck_out"])))
+        return out["ck_in"], out["ck_mlwe"], out["ck_out"]
+
+    def Commit(self, v, rnd):
+        """Commit(v) (prover.go:45-62) with injected randomness; v: [n][L] Montgomery."""
+        P = self.params
+        v = np.ascontiguousarray(v, np.uint64)
+        if v.shape[0] > P.rank:
+            raise RingoPanic("len(v) > params.rank")
+        sh = P.shapes()
+        o = {k: np.zeros(sh[k], np.uint64) for k in ["incom", "enc", "mlwe_out", "com"]}
+        args = [np.ascontiguousarray(rnd.last_row, np.uint64), np.ascontiguousarray(rnd.mask, np.uint64)]
+        en = np.ascontiguousarray(rnd.enc_noise, np.int64)
+        mn = np.ascontiguousarray(rnd.mlwe_noise, np.int64)
+        check(lib().rg_jindo_commit(self.h, ptr(v), v.shape[0], ptr(args[0]), ptr(args[1]), iptr(en), iptr(mn),
+                                    ptr(o["incom"]), ptr(o["enc"]), ptr(o["mlwe_out"]), ptr(o["com"])))
+        return Commitment(o["com"]), Opening(o["incom"], o["enc"], o["mlwe_out"])
+
+    def commit_dev(self, batch, v, nv, last_row, mask, enc_noise, mlwe_noise, incom, enc, mlwe, com, stream=None):
+        """rg_jindo_commit_dev on device buffers (tensors or int addresses)."""
+        check(lib().rg_jindo_commit_dev(self.h, batch, _addr(v), nv, _addr(last_row), _addr(mask), _addr(enc_noise),
+                                        _addr(mlwe_noise), _addr(incom), _addr(enc), _addr(mlwe), _addr(com),
+                                        _stream(stream)))
+
+
+def NewProver(params, crs):
+    return Prover(params, crs=crs)

@@ -1,0 +1,110 @@
+"""GPU parity: libringo's Jindo commit (rg_jindo_commit / rg_jindo_commit_dev) vs the C oracle
+(oracle/oracle.c, itself cross-checked against the big-int restatement), bit-exact on every
+output of Prover.Commit (jindo/prover.go:45-202): Opening.{InCommit, Encode, MLWE} and
+Commitment.Value, plus the CRS-derived commit key (entities.go:21-73).
+
+Shapes: tests/golden/jindo_params.json (jindo_test sizes, configs[2] 2^14, and the 3-prime
+examples/mult config).  Randomness is injected (tests/jindo_util.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import coracle as co
+import pyref
+from ringo import jindo
+from tests.jindo_util import make_randomness, make_v
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+PARAMS = json.load(open(os.path.join(HERE, "golden", "jindo_params.json")))
+
+
+def _setup(name):
+    P = PARAMS[name]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    return P, q, params
+
+
+def _oracle_commit(P, q, ck, v, rnd):
+    cj = co.CJindo(P, q)
+    return cj.commit(ck[0], ck[1], ck[2], v, rnd["last_row"], rnd["mask"], rnd["enc_noise"], rnd["mlwe_noise"])
+
+
+@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "mult_t8193_b12"])
+def test_commit_key_from_crs(name):
+    P, q, params = _setup(name)
+    prv = jindo.NewProver(params, b"Jindo!")
+    got = prv.commit_key()
+    want = pyref.commit_key(pyref.JindoParams(q, P["target_n"], P["batch"]), b"Jindo!")
+    for g, w in zip(got, want):
+        assert (g == np.array(w, dtype=np.uint64)).all()
+
+
+@pytest.mark.parametrize("name,nvs", [("t10_b1", [1024, 300, 33, 1]), ("t10_b8", [1024, 129]),
+                                      ("mult_t8193_b12", [8193, 700]), ("t14_b1", [16384, 5000])])
+def test_commit_matches_oracle(name, nvs):
+    P, q, params = _setup(name)
+    prv = jindo.NewProver(params, b"Jindo!")
+    ck = prv.commit_key()
+    for nv in nvs:
+        v = make_v(q, nv, seed=nv)
+        rnd = make_randomness(P, q, seed=nv + 7)
+        com, op = prv.Commit(v, jindo.Randomness(**rnd))
+        want = _oracle_commit(P, q, ck, v, rnd)
+        assert (op.Encode == want["enc"]).all(), (name, nv, "Encode")
+        assert (op.MLWE == want["mlwe"]).all(), (name, nv, "MLWE")
+        assert (op.InCommit == want["incom"]).all(), (name, nv, "InCommit")
+        assert (com.Value == want["com"]).all(), (name, nv, "Commitment")
+
+
+def test_commit_golden_digests():
+    """The jindo_test-size commit against the committed fixture digests."""
+    import hashlib
+    G = json.load(open(os.path.join(HERE, "golden", "jindo_commit_golden.json")))
+    P, q, params = _setup("t10_b1")
+    prv = jindo.NewProver(params, b"Jindo!")
+    ck = prv.commit_key()
+    assert [hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest() for x in ck] == G["ck"]
+    for nv, dig in G["cases"].items():
+        nv = int(nv)
+        v = make_v(q, nv, seed=nv)
+        rnd = make_randomness(P, q, seed=nv + 1)
+        com, op = prv.Commit(v, jindo.Randomness(**rnd))
+        got = {"incom": op.InCommit, "enc": op.Encode, "mlwe": op.MLWE, "com": com.Value}
+        for k, d in dig.items():
+            assert hashlib.sha256(np.ascontiguousarray(got[k]).tobytes()).hexdigest() == d, (nv, k)
+
+
+def test_commit_dev_batch_matches_single():
+    import torch
+    P, q, params = _setup("t10_b1")
+    prv = jindo.NewProver(params, b"Jindo!")
+    ck = prv.commit_key()
+    B, nv = 4, 1000
+    sh = params.shapes(B)
+    vs = np.stack([make_v(q, nv, seed=100 + b) for b in range(B)])
+    rnd = make_randomness(P, q, seed=5, batch=B)
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    dv, dl, dm, de, dn = t(vs), t(rnd["last_row"]), t(rnd["mask"]), t(rnd["enc_noise"]), t(rnd["mlwe_noise"])
+    outs = {k: torch.zeros(sh[k], dtype=torch.int64, device=dev) for k in ["incom", "enc", "mlwe_out", "com"]}
+    prv.commit_dev(B, dv, nv, dl, dm, de, dn, outs["incom"], outs["enc"], outs["mlwe_out"], outs["com"])
+    torch.cuda.synchronize()
+    for b in range(B):
+        want = _oracle_commit(P, q, ck, vs[b], {k: v[b] for k, v in rnd.items()})
+        assert (outs["com"][b].cpu().numpy().view(np.uint64) == want["com"]).all(), b
+        assert (outs["incom"][b].cpu().numpy().view(np.uint64) == want["incom"]).all(), b
+        assert (outs["enc"][b].cpu().numpy().view(np.uint64) == want["enc"]).all(), b
+        assert (outs["mlwe_out"][b].cpu().numpy().view(np.uint64) == want["mlwe"]).all(), b
+
+
+def test_commit_rank_panic():
+    P, q, params = _setup("t10_b1")
+    prv = jindo.NewProver(params, b"Jindo!")
+    v = make_v(q, P["rank"] + 1, seed=1)
+    rnd = make_randomness(P, q, seed=2)
+    with pytest.raises(Exception, match="len\\(v\\) > params.rank"):
+        prv.Commit(v, jindo.Randomness(**rnd))
