@@ -127,6 +127,68 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L)
 
 
+def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world):
+    """Device-resident batched commits (rg_jindo_commit_dev) at a BASELINE Jindo config.
+    The commit key is derived from the CRS on rank 0 and broadcast once over RCCL (xGMI)."""
+    from ringo import jindo
+    from ringo.shard import broadcast_commit_key
+    P = json.load(open(os.path.join(ROOT, "tests", "golden", "jindo_params.json")))[cfg_name]
+    fq = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, fq)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if world > 1:
+        if rank == 0:
+            ck = jindo.NewProver(params, b"Jindo!").commit_key()
+        else:
+            ck = tuple(np.zeros(s, np.uint64) for s in params.ck_shapes().values())
+        ck = broadcast_commit_key(ck, dist, device=dev)
+        prv = jindo.Prover(params, ck=ck)
+    else:
+        prv = jindo.NewProver(params, b"Jindo!")
+    L, nv = params.L, params.rank
+    sh = params.shapes(batch)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+
+    def elems(shape):  # uniform limbs, top limb < 2^(bits-2) so every value is < q
+        t = torch.randint(-(2 ** 63), 2 ** 63 - 1, shape, dtype=torch.int64, device=dev, generator=g)
+        top = fq >> (64 * (L - 1))
+        t[..., L - 1] &= (1 << max(top.bit_length() - 2, 1)) - 1
+        return t
+
+    v = elems((batch, nv, L))
+    last = elems(sh["last_row"])
+    last[:, -1, :] = 0
+    mask = elems(sh["mask"])
+    en = torch.randint(-4000, 4000, sh["enc_noise"], dtype=torch.int64, device=dev, generator=g)
+    mn = torch.randint(-40, 40, sh["mlwe_noise"], dtype=torch.int64, device=dev, generator=g)
+    outs = {k: torch.empty(sh[k], dtype=torch.int64, device=dev) for k in ["incom", "enc", "mlwe_out", "com"]}
+    stream = torch.cuda.current_stream()
+
+    def step():
+        prv.commit_dev(batch, v, nv, last, mask, en, mn, outs["incom"], outs["enc"], outs["mlwe_out"], outs["com"],
+                       stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ev = Events(torch, stream)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.time(step)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    nm = params.in_msis + params.mlwe
+    bytes_per_commit = 8 * (nv * L + params.dcmp * params.nqo * params.d + (params.cols + 1) * params.rows *
+                            params.nq * params.d + (params.cols + 1) * nm * params.nq * params.d +
+                            params.out_msis * params.nq * params.d)
+    return dict(wall_s=wall, kernel_ms=ev.total_ms(), commits=batch * steps, bytes_per_commit=bytes_per_commit)
+
+
 def cpu_baseline(q, L, logn, seconds):
     """C restatement (oracle/liboracle.so) fwd+inv on this host: bounded sample, all threads
     the OpenMP runtime gives it (OMP_NUM_THREADS)."""
@@ -210,6 +272,22 @@ def main():
                          "config": "configs[3]: fwd+inv negacyclic NTT, N=2^16, 255-bit Jindo prime, batch 64/GPU",
                          "achieved_GBs": 2 * N * 32 * r4["ntts"] / (r4["kernel_ms"] / 1000.0) / 1e9,
                          "selfcheck_fwd_inv_identity": r4["ok"]}
+    if not args.no_extra:
+        for cfg, jb in (("t14_b1", 64), ("t16_b4096", 16)):
+            jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world)
+            jms = jr["wall_s"] * 1000.0 / max(2, args.steps // 2)
+            if dist is not None:
+                t = torch.tensor([jms], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                jms = float(t[0])
+            key = "jindo_commit" if cfg == "t14_b1" else "jindo_commit_2e16"
+            out[key] = {"value": world * jb / (jms / 1000.0), "unit": "commits/s",
+                        "config": ("configs[2]: Jindo commit, targetN 2^14 (jindo_test params), q255" if cfg == "t14_b1"
+                                   else "configs[4] shape: Jindo commit, NewParameters(2^16, 4096), q255"),
+                        "batch_per_gpu": jb, "ms_per_batch": jms,
+                        "achieved_GBs": jr["bytes_per_commit"] * jr["commits"] / (jr["kernel_ms"] / 1000.0) / 1e9,
+                        "bytes_per_commit": jr["bytes_per_commit"],
+                        "randomness": "injected (device-generated integers); host Gaussian sampling not timed"}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(P63, 1, args.logn, args.cpu_seconds)
     if rank == 0:

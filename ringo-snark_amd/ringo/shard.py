@@ -1,0 +1,35 @@
+"""Multi-GPU layout for the hot path: one process per GPU (torch.distributed; backend "nccl"
+is RCCL on ROCm), independent polynomials / commitments sharded in contiguous ranges with no
+data-path collective, and ONE collective at setup: the commit key is broadcast
+from rank 0 over xGMI (or regenerated from the CRS per rank, which needs no collective)."""
+import numpy as np
+
+
+def shard_range(n_units, rank, world):
+    """Contiguous [lo, hi) slice of n_units owned by `rank` (sizes differ by at most one)."""
+    base, extra = divmod(n_units, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def broadcast_commit_key(ck, dist, device=None, src=0):
+    """Broadcast the three commit-key arrays (uint64, any shape) from `src` to every rank.
+
+    ck: tuple of numpy uint64 arrays on `src` (shapes must be known on every rank: pass
+    zero arrays of the right shape elsewhere).  Uses one flat buffer so the collective is a
+    single large transfer (xGMI links are point-to-point; one big message beats three).
+    Returns the arrays on every rank.
+    """
+    import torch
+    sizes = [a.size for a in ck]
+    flat = np.concatenate([np.ascontiguousarray(a, np.uint64).reshape(-1) for a in ck])
+    t = torch.from_numpy(flat.view(np.int64).copy())
+    if device is not None:
+        t = t.to(device)
+    dist.broadcast(t, src=src)
+    out = t.cpu().numpy().view(np.uint64)
+    res, off = [], 0
+    for a, n in zip(ck, sizes):
+        res.append(out[off:off + n].reshape(a.shape))
+        off += n
+    return tuple(res)
