@@ -21,6 +21,7 @@
 // All residues are canonical, so results are bit-exact against the reference's Lattigo
 // calls given the same primes (Lattigo conventions restated: see DESIGN.md, "parity").
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -75,18 +76,20 @@ __device__ __forceinline__ uint64_t sh_mul(uint64_t y, uint64_t w, uint64_t wp, 
 __device__ __forceinline__ uint64_t signed_residue(long long c, uint64_t q) {
   // setCoeffSigned (utils.go:49-61): c >= 0 -> c ; else Go's c%q + q (== q when q | c; the
   // following MForm maps that to 0 either way)
-  if (c >= 0) return (uint64_t)c % q;
+  if (c >= 0) return (uint64_t)c < q ? (uint64_t)c : (uint64_t)c % q;
   const uint64_t a = (uint64_t)(-(c + 1)) + 1;
-  return q - a % q;
+  return a < q ? q - a : q - a % q;
 }
 
 // d-point negacyclic NTT (Lattigo ordering: natural -> bit-reversed) of one limb held in LDS,
 // by `nt` threads (thread index `ti`); synchronises the whole workgroup between stages.
 __device__ void ntt_lds(uint64_t* p, int d, const ulonglong2* roots, uint64_t q, int ti, int nt, bool active) {
-  for (int m = 1, t = d >> 1; m < d; m <<= 1, t >>= 1) {
+  int lt = 0;
+  while ((2 << lt) < d) ++lt;  // log2(d/2)
+  for (int m = 1, t = d >> 1; m < d; m <<= 1, t >>= 1, --lt) {
     if (active) {
       for (int k = ti; k < (d >> 1); k += nt) {
-        const int i = k / t, j = 2 * i * t + (k % t);
+        const int i = k >> lt, j = (i << (lt + 1)) + (k & (t - 1));
         const ulonglong2 w = roots[m + i];
         const uint64_t u = p[j], v = sh_mul(p[j + t], w.x, w.y, q);
         p[j] = mod_add(u, v, q);
@@ -99,10 +102,10 @@ __device__ void ntt_lds(uint64_t* p, int d, const ulonglong2* roots, uint64_t q,
 // inverse (GS, bit-reversed -> natural), times d^-1
 __device__ void intt_lds(uint64_t* p, int d, const ulonglong2* roots, const RnsPrime& P, int ti, int nt, bool active) {
   const uint64_t q = P.q;
-  for (int m = d >> 1, t = 1; m >= 1; m >>= 1, t <<= 1) {
+  for (int m = d >> 1, t = 1, lt = 0; m >= 1; m >>= 1, t <<= 1, ++lt) {
     if (active) {
       for (int k = ti; k < (d >> 1); k += nt) {
-        const int i = k / t, j = 2 * i * t + (k % t);
+        const int i = k >> lt, j = (i << (lt + 1)) + (k & (t - 1));
         const ulonglong2 w = roots[m + i];
         const uint64_t u = p[j], v = p[j + t];
         p[j] = mod_add(u, v, q);
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         uint64_t sh = sh_mul(signed_residue(cs, q), P.r64, P.r64_sh, q);
         if (ks < 0) sh = mod_neg(sh, q);  // wrapped coefficients negate (:191-195)
         sh = mod_sub(sh, sh_mul(sm, P.bmod, P.bmod_sh, q), q);                   // :196
-        const uint64_t dm = sh_mul(dgk % q, P.r64, P.r64_sh, q);                 // MForm(digits) :198
+        const uint64_t dm = sh_mul(dgk, P.r64, P.r64_sh, q);  // MForm(digits) :198 (digit <= b < q)
         poly[l][k] = mod_add(dm, sh, q);                                          // :199
       }
     }
@@ -318,59 +321,128 @@ struct MacArgs {
   RnsPrime P[kMaxQ];
 };
 
-__device__ __forceinline__ void acc_add(uint64_t& lo, uint64_t& hi, uint32_t& top, uint64_t a, uint64_t b) {
-  uint64_t pl, ph;
-  mul_wide(a, b, pl, ph);
-  uint32_t c = 0;
-  lo = addc(lo, pl, c);
-  uint32_t c2 = 0;
-  hi = addc(hi, ph, c2);
-  uint32_t c3 = 0;
-  hi = addc(hi, (uint64_t)c, c3);
-  top += c2 + c3;
-}
+// acc += a * b as an exact multiword sum; WIDE keeps a third word (needed only when
+// (q-1)^2 * terms could reach 2^128: decided per launch on the host).
+template <bool WIDE>
+struct Acc {
+  uint64_t lo, hi;
+  uint32_t top;
+  __device__ __forceinline__ void zero() {
+    lo = hi = 0;
+    top = 0;
+  }
+  __device__ __forceinline__ void mac(uint64_t a, uint64_t b) {
+    uint64_t pl, ph;
+    mul_wide(a, b, pl, ph);
+    uint32_t c = 0;
+    lo = addc(lo, pl, c);
+    if constexpr (WIDE) {
+      uint32_t c2 = 0;
+      hi = addc(hi, ph, c2);
+      uint32_t c3 = 0;
+      hi = addc(hi, (uint64_t)c, c3);
+      top += c2 + c3;
+    } else {
+      hi += ph + c;
+    }
+  }
+  // (lo + hi 2^64 + top 2^128) * 2^-64 mod q = lo 2^-64 + hi + top 2^64
+  __device__ __forceinline__ uint64_t reduce(const RnsPrime& P) const {
+    const uint64_t q = P.q;
+    uint64_t r = sh_mul(lo, P.rinv, P.rinv_sh, q);
+    r = mod_add(r, sh_mul(hi, 1, P.one_sh, q), q);
+    if constexpr (WIDE) r = mod_add(r, sh_mul((uint64_t)top, P.r64, P.r64_sh, q), q);
+    return r;
+  }
+};
 
-template <int JB>
+// Thread = (column group of NC columns, limb*coeff).  Per term: JB commit-key words are loaded
+// once and reused for NC columns, NC data words reused for JB outputs (register tiling of the
+// per-(limb, coeff) modular GEMM  out[j][col] = sum_t A[j][t] B[t][col]).
+template <int JB, int NC, bool WIDE>
 __global__ __launch_bounds__(256) void mac_kernel(MacArgs a, int j0) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long per_col = (long long)a.nl * a.d;
-  if (gid >= a.ncols * per_col) return;
-  const long long col = gid / per_col;
+  const long long ngroups = (a.ncols + NC - 1) / NC;
+  if (gid >= ngroups * per_col) return;
+  const long long cg = gid / per_col;
   const int lk = (int)(gid % per_col);  // limb * d + coeff
   const int l = lk / a.d;
   const int J = min(JB, a.J - j0);
-  uint64_t lo[JB], hi[JB];
-  uint32_t top[JB];
+  const long long col0 = cg * NC;
+  const int nc = (int)min((long long)NC, a.ncols - col0);
+  Acc<WIDE> acc[NC][JB];
 #pragma unroll
-  for (int j = 0; j < JB; ++j) lo[j] = hi[j] = top[j] = 0;
-  const uint64_t* b1 = a.B1 + col * a.b1_col + lk;
-  for (int t = 0; t < a.T1; ++t) {
-    const uint64_t x = b1[t * a.b1_term];
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int j = 0; j < JB; ++j)
-      if (j < J) acc_add(lo[j], hi[j], top[j], a.A1[((long long)(j0 + j) * a.T1 + t) * per_col + lk], x);
-  }
-  if (a.T2) {
-    const uint64_t* b2 = a.B2 + col * a.b2_col + lk;
-    for (int t = 0; t < a.T2; ++t) {
-      const uint64_t x = b2[t * a.b2_term];
+    for (int j = 0; j < JB; ++j) acc[c][j].zero();
+  for (int set = 0; set < 2; ++set) {
+    const int T = set ? a.T2 : a.T1;
+    if (!T) continue;
+    const uint64_t* A = (set ? a.A2 : a.A1) + lk;
+    const uint64_t* Bp = (set ? a.B2 : a.B1) + lk;
+    const long long bcol = set ? a.b2_col : a.b1_col, bterm = set ? a.b2_term : a.b1_term;
+    for (int t = 0; t < T; ++t) {
+      uint64_t av[JB], bv[NC];
 #pragma unroll
-      for (int j = 0; j < JB; ++j)
-        if (j < J) acc_add(lo[j], hi[j], top[j], a.A2[((long long)(j0 + j) * a.T2 + t) * per_col + lk], x);
+      for (int j = 0; j < JB; ++j) av[j] = (j < J) ? A[((long long)(j0 + j) * T + t) * per_col] : 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) bv[c] = (c < nc) ? Bp[(col0 + c) * bcol + t * bterm] : 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < JB; ++j) acc[c][j].mac(av[j], bv[c]);
     }
   }
   const RnsPrime& P = a.P[l];
-  const uint64_t q = P.q;
 #pragma unroll
-  for (int j = 0; j < JB; ++j) {
-    if (j >= J) continue;
-    // (lo + hi 2^64 + top 2^128) * 2^-64 = lo 2^-64 + hi + top 2^64  (mod q)
-    uint64_t r = sh_mul(lo[j], P.rinv, P.rinv_sh, q);
-    r = mod_add(r, sh_mul(hi[j], 1, P.one_sh, q), q);
-    r = mod_add(r, sh_mul((uint64_t)top[j], P.r64, P.r64_sh, q), q);
-    if (a.C) r = mod_add(a.C[col * a.c_col + (long long)(j0 + j) * a.c_j + lk], r, q);
-    a.out[(col * a.J + j0 + j) * per_col + lk] = r;
+  for (int c = 0; c < NC; ++c) {
+    if (c >= nc) continue;
+    const long long col = col0 + c;
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      if (j >= J) continue;
+      uint64_t r = acc[c][j].reduce(P);
+      if (a.C) r = mod_add(a.C[col * a.c_col + (long long)(j0 + j) * a.c_j + lk], r, P.q);
+      a.out[(col * a.J + j0 + j) * per_col + lk] = r;
+    }
   }
+}
+
+constexpr int kMacNC = 4;
+
+template <int JB, bool WIDE>
+static rg_status launch_mac_jb(const MacArgs& m, int j0, hipStream_t st) {
+  const long long groups = (m.ncols + kMacNC - 1) / kMacNC;
+  const long long threads = groups * m.nl * m.d;
+  hipLaunchKernelGGL((mac_kernel<JB, kMacNC, WIDE>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, m, j0);
+  return check_launch("jindo mac");
+}
+
+template <bool WIDE>
+static rg_status launch_mac_w(const MacArgs& m, int jb, int j0, hipStream_t st) {
+  switch (jb) {
+    case 1: return launch_mac_jb<1, WIDE>(m, j0, st);
+    case 2: return launch_mac_jb<2, WIDE>(m, j0, st);
+    case 3: return launch_mac_jb<3, WIDE>(m, j0, st);
+    case 4: return launch_mac_jb<4, WIDE>(m, j0, st);
+    case 5: return launch_mac_jb<5, WIDE>(m, j0, st);
+    case 6: return launch_mac_jb<6, WIDE>(m, j0, st);
+    case 7: return launch_mac_jb<7, WIDE>(m, j0, st);
+    default: return launch_mac_jb<8, WIDE>(m, j0, st);
+  }
+}
+
+// J outputs split into ceil(J/8) launches of equal width
+static rg_status launch_mac(const MacArgs& m, hipStream_t st) {
+  uint64_t qmax = 0;
+  for (int l = 0; l < m.nl; ++l) qmax = std::max(qmax, m.P[l].q);
+  const double bits = 2.0 * log2((double)(qmax - 1)) + log2((double)(m.T1 + m.T2) + 1.0);
+  const bool wide = bits >= 127.5;
+  const int passes = (m.J + 7) / 8;
+  const int jb = (m.J + passes - 1) / passes;
+  for (int j0 = 0; j0 < m.J; j0 += jb) RG_TRY(wide ? launch_mac_w<true>(m, jb, j0, st) : launch_mac_w<false>(m, jb, j0, st));
+  return RG_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -433,7 +505,8 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
         const uint64_t qj = a.crt.q[j];
         uint64_t v = r[j];
         for (int kk = 0; kk < j; ++kk) {
-          const uint64_t xk = x[kk] >= qj ? x[kk] % qj : x[kk];
+          uint64_t xk = x[kk];
+          if (xk >= qj) xk = (xk - qj >= qj) ? xk % qj : xk - qj;  // ring primes share a bit size
           v = mod_sub(v, xk, qj);
           v = sh_mul(v, a.crt.inv[j][kk], a.crt.inv_sh[j][kk], qj);
         }
@@ -699,6 +772,10 @@ static rg_status validate(const rg_jindo_params* p) {
   if (p->in_msis < 1 || p->in_msis > kMaxJ || p->out_msis < 1 || p->out_msis > kMaxJ || p->mlwe < 0) return RG_ERR_INVALID;
   if (p->dcmp != (p->cols + 1) * p->in_msis) return RG_ERR_INVALID;
   if (p->base < 2 || (p->base >> 32)) return RG_ERR_INVALID;
+  for (int l = 0; l < p->nq; ++l)
+    if (p->q[l] <= p->base) return RG_ERR_INVALID;  // digits (<= b) are used as residues directly
+  for (int l = 0; l < p->nqo; ++l)
+    if (p->qo[l] <= p->base) return RG_ERR_INVALID;
   if (!(p->field_limbs == 1 || p->field_limbs == 2 || p->field_limbs == 4 || p->field_limbs == 7 ||
         p->field_limbs == 14))
     return RG_ERR_UNSUPPORTED;
@@ -822,13 +899,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   ma.c_j = (long long)nq * d;
   ma.out = J->s_com.as<uint64_t>();
   for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
-  {
-    const long long threads = ma.ncols * nq * d;
-    for (int j0 = 0; j0 < ma.J; j0 += 8) {
-      hipLaunchKernelGGL(mac_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ma, j0);
-      RG_TRY(check_launch("jindo mac"));
-    }
-  }
+  RG_TRY(launch_mac(ma, st));
   // 4. inner round -> Opening.InCommit (column i, j -> index i*inMSIS + j)
   RoundArgs ra;
   memset(&ra, 0, sizeof(ra));
@@ -861,13 +932,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   mo.b1_term = (long long)nqo * d;
   mo.out = J->s_ocom.as<uint64_t>();
   for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
-  {
-    const long long threads = mo.ncols * nqo * d;
-    for (int j0 = 0; j0 < mo.J; j0 += 8) {
-      hipLaunchKernelGGL(mac_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, mo, j0);
-      RG_TRY(check_launch("jindo mac(out)"));
-    }
-  }
+  RG_TRY(launch_mac(mo, st));
   RoundArgs ro = ra;
   ro.cut = p.log_out_cut;
   ro.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);

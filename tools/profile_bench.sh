@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of the default bench command, then PMC passes (each its own
+# run, --kernel-trace only).  Usage (on the GPU box): tools/profile_bench.sh <outdir> [bench args]
+set -e
+OUT=${1:-$GRAFT_REPO_ROOT/gpurun_out/prof}
+shift || true
+ARGS=${@:---steps 4 --warmup 1 --no-cpu}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/bench_under_trace.json 2> $OUT/trace.err
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > /dev/null 2>$OUT/p$i.err || { echo "pmc pass $i failed"; exit 1; }
+done
