@@ -839,12 +839,263 @@ static rg_status dispatch_r2(bool col, const NttArgs<L>& a, hipStream_t st) {
 
 namespace rg {
 
+}  // namespace rg
+
+// ----------------------------------------------------------------------------------------
+// Radix-8 pass for single-word Shoup fields (P = 8 as rounds of 3 + 3 + 2 bits).
+// 8 points per thread (16 VGPRs of data instead of 32) and 512-thread workgroups holding 16
+// sub-transforms: the register file admits ~8 waves per SIMD, which is what hides the
+// dependent-issue latency of 64-bit integer multiply chains (the radix-16 pass measured
+// ~6 cycles per VALU instruction at 2 waves/SIMD).  Two LDS exchanges per pass instead of
+// one.  Lane mapping as in ntt_r2_kernel: COL s fastest (16 columns -> 128 B runs),
+// ROW t fastest (32 consecutive points).  LDS images per exchange: see ntt_r8_kernel.
+// ----------------------------------------------------------------------------------------
+namespace rg {
+
+template <int RK, bool INV, bool SCALE, bool QLO1>
+__device__ __forceinline__ void r8_round(const NttArgs<1>& a, uint64_t (&e)[8], int LO, long long hi, int t,
+                                         bool uniform) {
+  // window [LO, LO+RK) of x; the thread's 8 registers hold NG = 8 >> RK groups of 2^RK
+  // points: register r = g * 2^RK + y, group index g extends the thread's other bits.
+  constexpr int NG = 8 >> RK;
+  constexpr int NPK = 1 << RK;
+  const int HI = LO + RK;
+  const uint64_t q = a.F.q[0];
+#pragma unroll
+  for (int sp = 0; sp < RK; ++sp) {
+    const int gp = INV ? (7 - (LO + sp)) : ((8 - HI) + sp);
+    const bool last = INV && SCALE && (a.G0 + gp == 0);
+    const int half = INV ? (1 << sp) : (NPK >> (sp + 1));
+    const int nblk = NPK / (2 * half);
+    uint64_t w[4], wp[4];
+    // twiddles for the 4 butterflies of this stage (k = g * (NPK/2) + blk * half + u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int g = k / (NPK / 2), kk = k % (NPK / 2), blk = kk / half;
+      if (k % half) {
+        w[k] = w[k - 1];
+        wp[k] = wp[k - 1];
+        continue;
+      }
+      // bits of x above the window: o = t * NG + g, o_high = o >> LO
+      const int o = t * NG + g;
+      const long long ohigh = o >> LO;
+      long long idx = INV ? ((1LL << (a.G0 + gp)) + (hi << gp) + (ohigh << (RK - sp - 1)) + blk)
+                          : ((1LL << (a.G0 + gp)) + (hi << gp) + (ohigh << sp) + blk);
+      if (last) {
+        w[k] = a.w1n[0];
+        wp[k] = a.w1n_sh;
+      } else {
+        if (uniform) idx = __builtin_amdgcn_readfirstlane((int)idx);
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[idx];
+        w[k] = v.x;
+        wp[k] = v.y;
+      }
+      (void)nblk;
+    }
+    uint64_t r[4];
+    if constexpr (!INV) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int g = k / (NPK / 2), kk = k % (NPK / 2), blk = kk / half, u = kk % half;
+        const int i1 = g * NPK + blk * 2 * half + u + half;
+        r[k] = reduce2q(shoup_lazy<QLO1>(e[i1], w[k], wp[k], q), q);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int g = k / (NPK / 2), kk = k % (NPK / 2), blk = kk / half, u = kk % half;
+        const int i0 = g * NPK + blk * 2 * half + u, i1 = i0 + half;
+        const uint64_t x0 = e[i0];
+        e[i0] = addmod63(x0, r[k], q);
+        e[i1] = submod63(x0, r[k], q);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int g = k / (NPK / 2), kk = k % (NPK / 2), blk = kk / half, u = kk % half;
+        const int i0 = g * NPK + blk * 2 * half + u, i1 = i0 + half;
+        const uint64_t x0 = e[i0], x1 = e[i1];
+        e[i0] = addmod63(x0, x1, q);
+        r[k] = submod63(x0, x1, q);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int g = k / (NPK / 2), kk = k % (NPK / 2), blk = kk / half, u = kk % half;
+        const int i0 = g * NPK + blk * 2 * half + u, i1 = i0 + half;
+        e[i1] = reduce2q(shoup_lazy<QLO1>(r[k], w[k], wp[k], q), q);
+        if (last) e[i0] = shoup_mul(e[i0], a.nsc[0], a.nsc_sh, q);
+      }
+    }
+  }
+}
+
+template <bool INV, bool SCALE, bool COL, bool QLO1, bool PF>
+__global__ __launch_bounds__(512) void ntt_r8_kernel(NttArgs<1> a) {
+  constexpr int SW = 16, PADN = 288;
+  __shared__ uint64_t lds[SW * PADN];
+  const int tid = threadIdx.x;
+  const int s = COL ? (tid & 15) : (tid >> 5);
+  const int t = COL ? (tid >> 4) : (tid & 31);
+  const int logN = a.logN;
+  const int logS = logN - a.G0 - 8;
+  const int rowshift = logN - a.G0;
+  const long long ntiles = a.total_sub / SW;
+  const uint32_t lane_off = COL ? (uint32_t)s : ((uint32_t)s << rowshift);
+  const int xshift = COL ? logS : 0;
+  auto tile_base = [&](long long tile) -> long long {
+    const long long sub0 = tile * SW;
+    return COL ? (((sub0 >> logS) << rowshift) + (sub0 & ((1LL << logS) - 1))) : (sub0 << rowshift);
+  };
+  // LDS image per exchange (bank-conflict-free for both patterns of the exchange, checked
+  // against the ds_read_b64 / ds_write_b64 lane-group model):
+  //   COL: transposed [x][s] image, 16 x + s + 16 (x >> 3) -- every pattern
+  //   ROW: [s][x] image; {H,M}: x + 4 (x >> 5); {M,L}: x + (x >> 3); {L,H}: x + (x >> 5)
+  enum { HM, ML, LH };
+  auto lpos = [&](int x, int ph) {
+    if (COL) return 16 * x + s + 16 * (x >> 3);
+    return s * PADN + x + (ph == HM ? 4 * (x >> 5) : ph == ML ? (x >> 3) : (x >> 5));
+  };
+  // point patterns: H = top window x = t + 32 y;  M = x = (t>>2)<<5 | y<<2 | (t&3);
+  //                 L = bottom window, 2 groups: x = 8t + 4g + y   (register r = 4g + y)
+  auto xH = [&](int y) { return t + 32 * y; };
+  auto xM = [&](int y) { return ((t >> 2) << 5) | (y << 2) | (t & 3); };
+  auto xL = [&](int r) { return 8 * t + r; };
+  // the first round's raw global loads (coalesced pattern): forward H; inverse COL L, ROW H
+  constexpr bool LOAD_L = INV && COL;
+  auto gload = [&](uint64_t (&r)[8], long long tile) {
+    const uint64_t* gin = a.in + tile_base(tile);
+#pragma unroll
+    for (int y = 0; y < 8; ++y) r[y] = gin[((uint32_t)(LOAD_L ? xL(y) : xH(y)) << xshift) + lane_off];
+  };
+  const bool uni = COL;
+  uint64_t e[8], nx[8];
+  long long tile = blockIdx.x;
+  if (PF && tile < ntiles) gload(e, tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const long long nt = tile + gridDim.x;
+    if (!PF) gload(e, tile);
+    if (PF && nt < ntiles) gload(nx, nt);  // next tile's HBM reads overlap this tile's butterflies
+    const long long hi = COL ? 0 : ((tile * SW + s) & ((1LL << a.G0) - 1));
+    uint64_t* gout = a.out + tile_base(tile);
+    if (INV && !COL) {  // ROW inverse: loaded in H pattern, transpose to L through LDS
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xH(y), LH)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), LH)];
+      __syncthreads();
+    }
+    if (!INV) {
+      r8_round<3, false, SCALE, QLO1>(a, e, 5, hi, t, uni);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xH(y), HM)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), HM)];
+      r8_round<3, false, SCALE, QLO1>(a, e, 2, hi, t, false);
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), ML)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), ML)];
+      r8_round<2, false, SCALE, QLO1>(a, e, 0, hi, t, false);
+      if (COL) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) gout[((uint32_t)xL(r) << xshift) + lane_off] = e[r];
+      } else {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) lds[lpos(xL(r), LH)] = e[r];
+        __syncthreads();
+#pragma unroll
+        for (int y = 0; y < 8; ++y) gout[(uint32_t)xH(y) + lane_off] = lds[lpos(xH(y), LH)];
+      }
+    } else {
+      r8_round<2, true, SCALE, QLO1>(a, e, 0, hi, t, false);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) lds[lpos(xL(r), ML)] = e[r];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), ML)];
+      r8_round<3, true, SCALE, QLO1>(a, e, 2, hi, t, false);
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), HM)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xH(y), HM)];
+      r8_round<3, true, SCALE, QLO1>(a, e, 5, hi, t, uni);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) gout[((uint32_t)xH(y) << xshift) + lane_off] = e[y];
+    }
+    __syncthreads();  // LDS reuse by the next tile
+    if (PF) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = nx[y];
+    }
+  }
+}
+
+template <bool INV, bool SCALE, bool COL, bool QLO1, bool PF>
+static rg_status launch_r8_pf(const NttArgs<1>& a, hipStream_t st) {
+  const long long ntiles = a.total_sub / 16;
+  if (!PF) {  // one tile per workgroup
+    hipLaunchKernelGGL((ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>), dim3((unsigned)ntiles), dim3(512), 0, st, a);
+    return check_launch("ntt_r8");
+  }
+  static int cap = 0;
+  if (!cap) {  // persistent grid: the resident capacity (RINGO_NTT_WG_PER_CU overrides)
+    int per_cu = 0, dev = 0, cus = 256;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>, 512, 0);
+    const char* e = getenv("RINGO_NTT_WG_PER_CU");
+    if (e) per_cu = atoi(e);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    cap = (per_cu > 0 ? per_cu : 1) * cus;
+  }
+  const long long grid = ntiles < cap ? ntiles : cap;
+  hipLaunchKernelGGL((ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>), dim3((unsigned)grid), dim3(512), 0, st, a);
+  return check_launch("ntt_r8");
+}
+
+template <bool INV, bool SCALE, bool COL, bool QLO1>
+static rg_status launch_r8_q(const NttArgs<1>& a, hipStream_t st) {
+  static const int pf = getenv("RINGO_NTT_R8_PF") ? atoi(getenv("RINGO_NTT_R8_PF")) : 0;
+  return pf ? launch_r8_pf<INV, SCALE, COL, QLO1, true>(a, st)
+                               : launch_r8_pf<INV, SCALE, COL, QLO1, false>(a, st);
+}
+
+template <bool INV, bool SCALE, bool COL>
+static rg_status launch_r8(const NttArgs<1>& a, hipStream_t st) {
+  return a.qlo1 ? launch_r8_q<INV, SCALE, COL, true>(a, st) : launch_r8_q<INV, SCALE, COL, false>(a, st);
+}
+
+// RINGO_NTT_KERNEL=r2 selects the radix-16 pass instead (A/B switch)
+static inline bool use_r8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RINGO_NTT_KERNEL");
+    v = (e && e[0] == 'r' && e[1] == '2') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+}  // namespace rg
+
+namespace rg {
+
 template <int L, bool SHOUP>
 static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
   const size_t N = (size_t)1 << p.logN;
   const size_t poly_u64 = N * L;
   // chunk the batch so the pass-to-pass intermediate stays in the 256 MiB Infinity Cache
-  size_t chunk = std::max<size_t>(1, (size_t)(96ull << 20) / (poly_u64 * 8));
+  static size_t chunk_bytes = 0;
+  if (!chunk_bytes) {  // RINGO_NTT_CHUNK_MB overrides the Infinity-Cache-sized chunk (tuning)
+    const char* e = getenv("RINGO_NTT_CHUNK_MB");
+    chunk_bytes = (size_t)(e ? atoi(e) : 192) << 20;
+  }
+  size_t chunk = std::max<size_t>(1, chunk_bytes / (poly_u64 * 8));
   if (p.npasses == 1) chunk = p.batch;
   NttArgs<L> a;
   fill_args<L>(a, p);
@@ -861,6 +1112,18 @@ static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
       const int logS = p.logN - ps.G0 - ps.P;
       if (RadixOf<L>::value == 4 && ps.P == 8 && (logS == 0 || logS >= 4) && (a.total_sub % 16) == 0) {
         const bool col = logS >= 4;
+        if constexpr (L == 1 && SHOUP) {
+          if (use_r8()) {
+            if (!p.inv)
+              s = col ? launch_r8<false, false, true>(a, st) : launch_r8<false, false, false>(a, st);
+            else if (ps.G0 == 0)
+              s = col ? launch_r8<true, true, true>(a, st) : launch_r8<true, true, false>(a, st);
+            else
+              s = col ? launch_r8<true, false, true>(a, st) : launch_r8<true, false, false>(a, st);
+            RG_TRY(s);
+            continue;
+          }
+        }
         if (!p.inv)
           s = dispatch_r2<L, false, SHOUP, false>(col, a, st);
         else if (ps.G0 == 0)
@@ -907,4 +1170,5 @@ static rg_status run_stages(const NttLaunch& p, hipStream_t st) {
 }
 
 }  // namespace rg
+
 
