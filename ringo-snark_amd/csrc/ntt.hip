@@ -201,7 +201,11 @@ static rg_status run(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t 
   p.npasses = (int)t->passes.size();
   p.batch = batch;
   switch (t->f.L) {
-    case 1: return ntt_run_L1(p, st);
+    case 1: {
+      bool done = false;
+      RG_TRY(ntt64_run(p, st, &done));
+      return done ? RG_OK : ntt_run_L1(p, st);
+    }
     case 2: return ntt_run_L2(p, st);
     case 4: return ntt_run_L4(p, st);
     case 7: return ntt_run_L7(p, st);

@@ -1,0 +1,382 @@
+// ntt64.hpp -- single-word (q < 2^64/3, L = 1) NTT arithmetic for gfx950: lazy butterflies.
+//
+// Values between butterfly stages live in [0, 2q) ("Harvey" lazy form); only the last stage of
+// a transform maps them to the canonical residues the reference produces (gnark fully reduces,
+// jindo/internal/zp/element.go:397-466), so every output limb is bit-identical to ntt.go.
+// The twiddle product is Shoup's precomputed-quotient multiply, exact for any 64-bit input:
+//   wp = floor(w 2^64 / q),  qh = floor(y wp / 2^64),  y w - qh q  in [0, 2q).
+// q mod 2^32 == 1 (every jindo-modulus prime: p - 1 = b^(2^e) with b even) turns lo64(qh q)
+// into qh + ((qh_lo q_hi) << 32): one 32-bit multiply instead of three.
+// Cost model (tools/ubench, MI355X): 32-bit multiplies, 64-bit shifts/adds and carry ops issue
+// at ~4.4 cycles per wave64 instruction, plain v_add/v_sub/v_and/v_mov at ~2.4; a butterfly is
+// 8 multiplies + ~13 adds/selects.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "field.hpp"
+
+namespace rg {
+
+struct Q64 {
+  uint64_t q, q2;  // q, 2q (2q < 2^64 needs q < 2^63; the lazy add below needs q < 2^64/3)
+  uint32_t qhi;    // q >> 32
+  uint32_t qlo1;   // q mod 2^32 == 1
+};
+
+inline Q64 make_q64(uint64_t q) {
+  Q64 Q;
+  Q.q = q;
+  Q.q2 = 2 * q;
+  Q.qhi = (uint32_t)(q >> 32);
+  Q.qlo1 = (uint32_t)q == 1u;
+  return Q;
+}
+
+#if defined(__HIPCC__)
+
+// y * w mod q in [0, 2q), exact Shoup for any y < 2^64
+template <bool QLO1>
+__device__ __forceinline__ uint64_t shoup2(uint64_t y, uint64_t w, uint64_t wp, const Q64& Q) {
+  const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
+  const uint32_t p0 = (uint32_t)wp, p1 = (uint32_t)(wp >> 32);
+  // qh = hi64(y * wp): mid = y0 p1 + y1 p0 + hi(y0 p0) < 2^65 carries at most once
+  unsigned long long c1, c2;
+  const uint64_t mid0 = __builtin_addcll((uint64_t)y0 * p1, (uint64_t)y1 * p0, 0ull, &c1);
+  const uint64_t mid = __builtin_addcll(mid0, (uint64_t)__umulhi(y0, p0), 0ull, &c2);
+  const uint64_t qh = (uint64_t)y1 * p1 + ((mid >> 32) | ((uint64_t)(c1 | c2) << 32));
+  const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+  if constexpr (QLO1) {
+    const uint64_t l = (uint64_t)y0 * w0;
+    const uint32_t hi = (uint32_t)(l >> 32) + y0 * w1 + y1 * w0 - (uint32_t)qh * Q.qhi;
+    return (((uint64_t)hi << 32) | (uint32_t)l) - qh;
+  } else {
+    return y * w - qh * Q.q;
+  }
+}
+
+// [0, 4q) sum as (value mod 2^64, carry) -> [0, 2q)
+__device__ __forceinline__ uint64_t lazy_add(uint64_t x, uint64_t y, const Q64& Q) {
+  unsigned long long c, b;
+  const uint64_t s = __builtin_addcll(x, y, 0ull, &c);
+  const uint64_t t = __builtin_subcll(s, Q.q2, 0ull, &b);
+  return (c | (b ^ 1ull)) ? t : s;
+}
+// x - y + 2q (x, y in [0, 2q)) -> [0, 2q)
+__device__ __forceinline__ uint64_t lazy_sub(uint64_t x, uint64_t y, const Q64& Q) {
+  unsigned long long b;
+  const uint64_t d = __builtin_subcll(x, y, 0ull, &b);
+  return b ? d + Q.q2 : d;
+}
+// [0, 2q) -> [0, q)
+__device__ __forceinline__ uint64_t canon(uint64_t x, const Q64& Q) {
+  unsigned long long b;
+  const uint64_t t = __builtin_subcll(x, Q.q, 0ull, &b);
+  return b ? x : t;
+}
+
+// Cooley-Tukey (ntt.go:254-259): (x, y) <- (x + w y, x - w y), lazy in and out
+template <bool QLO1 = true>
+__device__ __forceinline__ void fwd_bfly_lazy(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, const Q64& Q) {
+  const uint64_t t = shoup2<QLO1>(y, w, wp, Q);
+  const uint64_t a = x;
+  x = lazy_add(a, t, Q);
+  y = lazy_sub(a, t, Q);
+}
+// Gentleman-Sande (ntt.go:365-370): (x, y) <- (x + y, (x - y) w), lazy in and out
+template <bool QLO1 = true>
+__device__ __forceinline__ void inv_bfly_lazy(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, const Q64& Q) {
+  const uint64_t a = x, b = y;
+  x = lazy_add(a, b, Q);
+  y = shoup2<QLO1>(lazy_sub(a, b, Q), w, wp, Q);
+}
+
+
+// ---- explicit-carry forms (VOP3b carry outputs in SGPR lane masks; the compiler keeps the
+// 32-bit halves of 64-bit values as sub-registers, so no pair is ever rebuilt) ----
+typedef unsigned long long lmask;  // wave64 lane mask (SGPR pair)
+
+__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, lmask& co) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, lmask& co) {
+  uint32_t d;
+  asm("v_add_co_u32 %0, %1, %2, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, lmask ci, lmask& co) {
+  uint32_t d;
+  asm("v_addc_co_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci));
+  return d;
+}
+__device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, lmask& bo) {
+  uint32_t d;
+  asm("v_sub_co_u32 %0, %1, %2, %3" : "=v"(d), "=s"(bo) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t subb_co(uint32_t a, uint32_t b, lmask bi, lmask& bo) {
+  uint32_t d;
+  asm("v_subb_co_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(bo) : "v"(a), "v"(b), "s"(bi));
+  return d;
+}
+__device__ __forceinline__ uint32_t sel(lmask m, uint32_t if1, uint32_t if0) {
+  uint32_t d;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(d) : "v"(if0), "v"(if1), "s"(m));
+  return d;
+}
+__device__ __forceinline__ uint64_t pk(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+__device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+
+// Shoup y * w mod q in [0, 2q), q mod 2^32 == 1; nqhi = -(q >> 32) mod 2^32
+__device__ __forceinline__ uint64_t shoup_x(uint64_t y, uint64_t w, uint64_t wp, uint32_t nqhi) {
+  const uint32_t y0 = lo32(y), y1 = hi32(y), p0 = lo32(wp), p1 = hi32(wp);
+  lmask cb, k;
+  const uint64_t a = (uint64_t)y0 * p1 + __umulhi(y0, p0);   // < 2^64
+  const uint64_t b = mad_co(y1, p0, a, cb);                  // y1 p0 + a, carry into 2^96
+  const uint64_t c = (uint64_t)y1 * p1 + hi32(b);            // < 2^64 (qh fits)
+  const uint32_t qh0 = lo32(c);
+  const uint32_t qh1 = addc_co(hi32(c), 0u, cb, k);
+  const uint64_t l = (uint64_t)y0 * lo32(w);
+  const uint32_t hi = hi32(l) + y0 * hi32(w) + y1 * lo32(w) + qh0 * nqhi;
+  lmask br;
+  const uint32_t r0 = sub_co(lo32(l), qh0, br);
+  const uint32_t r1 = subb_co(hi, qh1, br, k);
+  return pk(r0, r1);
+}
+// (x, y) <- (x + w y, x - w y), lazy [0, 2q) in and out; q2 = 2q
+__device__ __forceinline__ void fwd_bfly_x(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, uint64_t q2,
+                                           uint32_t nqhi) {
+  const uint64_t t = shoup_x(y, w, wp, nqhi);
+  lmask c, c2, b, b2, e, e2;
+  const uint32_t s0 = add_co(lo32(x), lo32(t), c);
+  const uint32_t s1 = addc_co(hi32(x), hi32(t), c, c2);
+  const uint32_t u0 = sub_co(s0, lo32(q2), b);
+  const uint32_t u1 = subb_co(s1, hi32(q2), b, b2);
+  const lmask m = c2 | ~b2;  // s >= 2q (65-bit)
+  const uint32_t d0 = sub_co(lo32(x), lo32(t), e);
+  const uint32_t d1 = subb_co(hi32(x), hi32(t), e, e2);
+  const uint64_t d = pk(d0, d1);
+  const uint64_t f = d + q2;
+  x = pk(sel(m, u0, s0), sel(m, u1, s1));
+  y = pk(sel(e2, lo32(f), d0), sel(e2, hi32(f), d1));
+}
+
+
+// (x, y) <- (x + y, (x - y) w), lazy [0, 2q) in and out
+__device__ __forceinline__ void inv_bfly_x(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, uint64_t q2,
+                                           uint32_t nqhi) {
+  lmask c, c2, b, b2, e, e2;
+  const uint32_t s0 = add_co(lo32(x), lo32(y), c);
+  const uint32_t s1 = addc_co(hi32(x), hi32(y), c, c2);
+  const uint32_t u0 = sub_co(s0, lo32(q2), b);
+  const uint32_t u1 = subb_co(s1, hi32(q2), b, b2);
+  const lmask m = c2 | ~b2;
+  const uint32_t d0 = sub_co(lo32(x), lo32(y), e);
+  const uint32_t d1 = subb_co(hi32(x), hi32(y), e, e2);
+  const uint64_t d = pk(d0, d1);
+  const uint64_t f = d + q2;
+  x = pk(sel(m, u0, s0), sel(m, u1, s1));
+  y = shoup_x(pk(sel(e2, lo32(f), d0), sel(e2, hi32(f), d1)), w, wp, nqhi);
+}
+// [0, 2q) -> [0, q)
+__device__ __forceinline__ uint64_t canon_x(uint64_t x, uint64_t q) {
+  lmask b, b2;
+  const uint32_t t0 = sub_co(lo32(x), lo32(q), b);
+  const uint32_t t1 = subb_co(hi32(x), hi32(q), b, b2);
+  return pk(sel(b2, lo32(x), t0), sel(b2, hi32(x), t1));
+}
+
+// ----------------------------------------------------------------------------------------
+// Pass kernel: 8 consecutive radix-2 stages [G0, G0+8) of a 2^logN-point transform, as 2^(logN-8)
+// independent 256-point sub-transforms per polynomial whose points sit at stride S =
+// 2^(logN-G0-8): COL (S >= 16, G0 = 0) or ROW (S = 1).  A 512-thread workgroup owns a tile of
+// 16 sub-transforms x 256 points = 32 KiB; each thread holds 8 points in registers and runs
+// three rounds of 3 + 3 + 2 stages with two LDS exchanges (plus one transpose for coalesced
+// ROW stores/loads).  Index algebra (ntt.go:98-115 forward, :357-466 inverse): local stage k
+// combines bit b = 7-k of the in-sub-transform index x and uses
+//     tw[2^(G0+k) + (hi << k) + (x >> (b+1))],   hi = sub-transform prefix (ROW: row index).
+// Register patterns per round (t = lane's slot, y / r = register):
+//     H: x = t + 32 y   (window bits [5,8))       M: x = (t>>2)<<5 | y<<2 | (t&3)   (bits [2,5))
+//     L: x = 8 t + r    (window bits [0,2), r>>2 = x bit 2)
+// ----------------------------------------------------------------------------------------
+struct Ntt64Args {
+  const uint64_t* in;
+  uint64_t* out;
+  const uint64_t* tw;  // (w, floor(w 2^64 / q)) pairs, forward or inverse table, [N][2]
+  uint64_t q, q2;
+  uint32_t nqhi, pad_;
+  uint64_t ninv, ninv_p;  // N^-1 and its Shoup quotient (inverse, last stage)
+  uint64_t w1n, w1n_p;    // twInv[1] N^-1
+  long long total_sub;    // batch * 2^(logN - 8)
+  int logN, G0;
+};
+
+// PROBE (tuning only; production = 0): 1 = twiddles from registers (no table loads),
+// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both
+template <int RK, int LO, int PAT, bool INV, bool SCALE, int PROBE = 0>
+__device__ __forceinline__ void ntt64_round(const Ntt64Args& a, uint64_t (&e)[8], long long hi, int t, bool uniform) {
+  // pat: 0 = H, 1 = M, 2 = L.  x(rho) for register rho of this thread:
+  auto xof = [&](int rho) -> int {
+    if (PAT == 0) return t + 32 * rho;
+    if (PAT == 1) return ((t >> 2) << 5) | (rho << 2) | (t & 3);
+    return 8 * t + rho;
+  };
+  constexpr int NPK = 1 << RK;  // points per group
+#pragma unroll
+  for (int sp = 0; sp < RK; ++sp) {
+    // forward: window bits processed top-down; inverse: bottom-up
+    const int bw = INV ? sp : (RK - 1 - sp);  // bit within the window
+    const int b = LO + bw;                     // bit of x
+    const int k = 7 - b;                       // local stage
+    const int half = 1 << bw;
+    const bool last = INV && SCALE && k == 0;  // SCALE: this pass holds global stage 0
+    uint64_t w[4], wp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // j-th pair: rho0 has bit bw clear
+      const int grp = j / (NPK / 2), jj = j % (NPK / 2);
+      const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
+      // pairs that share x >> (b+1) reuse the twiddle of the previous pair
+      const int hb = (jj & (half - 1)) != 0;
+      if (hb) {
+        w[j] = w[j - 1];
+        wp[j] = wp[j - 1];
+        continue;
+      }
+      if (last) {
+        w[j] = a.w1n;
+        wp[j] = a.w1n_p;
+        continue;
+      }
+      long long idx = (1LL << (a.G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
+      if (uniform) idx = __builtin_amdgcn_readfirstlane((int)idx);
+      if constexpr (PROBE & 1) {
+        w[j] = a.w1n + (uint64_t)idx;
+        wp[j] = a.w1n_p;
+        continue;
+      }
+      const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[idx];
+      w[j] = v.x;
+      wp[j] = v.y;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int grp = j / (NPK / 2), jj = j % (NPK / 2);
+      const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
+      const int rho1 = rho0 + half;
+      if constexpr ((PROBE & 2) != 0) {
+        e[rho0] += e[rho1] ^ w[j] ^ wp[j];
+      } else if constexpr (!INV) {
+        fwd_bfly_x(e[rho0], e[rho1], w[j], wp[j], a.q2, a.nqhi);
+      } else {
+        inv_bfly_x(e[rho0], e[rho1], w[j], wp[j], a.q2, a.nqhi);
+        if (last) e[rho0] = shoup_x(e[rho0], a.ninv, a.ninv_p, a.nqhi);
+      }
+    }
+  }
+}
+
+// CANON: map the outputs to [0, q) (last pass of a transform); SCALE: inverse with the fused
+// N^-1 (COL pass of the inverse, global stage 0 inside)
+template <bool INV, bool COL, bool SCALE, bool CANON, int MINW, int PROBE = 0>
+__global__ __launch_bounds__(512, MINW) void ntt64_pass(Ntt64Args a) {
+  constexpr int SW = 16, PADN = 288;
+  __shared__ uint64_t lds[SW * PADN];
+  const int tid = threadIdx.x;
+  const int s = COL ? (tid & 15) : (tid >> 5);
+  const int t = COL ? (tid >> 4) : (tid & 31);
+  const int logS = a.logN - a.G0 - 8;
+  const int rowshift = a.logN - a.G0;
+  const long long ntiles = a.total_sub / SW;
+  const uint32_t lane_off = COL ? (uint32_t)s : ((uint32_t)s << rowshift);
+  const int xshift = COL ? logS : 0;
+  // LDS images: COL: transposed [x][s], 16 x + s + 16 (x >> 3); ROW: [s][x] + per-exchange pad
+  enum { HM, ML, LH };
+  auto lpos = [&](int x, int ph) {
+    if (COL) return 16 * x + s + 16 * (x >> 3);
+    return s * PADN + x + (ph == HM ? 4 * (x >> 5) : ph == ML ? (x >> 3) : (x >> 5));
+  };
+  auto xH = [&](int y) { return t + 32 * y; };
+  auto xM = [&](int y) { return ((t >> 2) << 5) | (y << 2) | (t & 3); };
+  auto xL = [&](int r) { return 8 * t + r; };
+  constexpr bool LOAD_L = INV && COL;  // inverse COL starts in the L pattern
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long sub0 = tile * SW;
+    const long long base = COL ? (((sub0 >> logS) << rowshift) + (sub0 & ((1LL << logS) - 1))) : (sub0 << rowshift);
+    const uint64_t* gin = a.in + base;
+    uint64_t* gout = a.out + base;
+    const long long hi = COL ? 0 : ((sub0 + s) & ((1LL << a.G0) - 1));
+    uint64_t e[8];
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = gin[((uint32_t)(LOAD_L ? xL(y) : xH(y)) << xshift) + lane_off];
+    if (!INV) {
+      ntt64_round<3, 5, 0, false, false, PROBE>(a, e, hi, t, COL);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xH(y), HM)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), HM)];
+      ntt64_round<3, 2, 1, false, false, PROBE>(a, e, hi, t, false);
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), ML)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), ML)];
+      ntt64_round<2, 0, 2, false, false, PROBE>(a, e, hi, t, false);
+      if (CANON) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
+      }
+      if (COL) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) gout[((uint32_t)xL(r) << xshift) + lane_off] = e[r];
+      } else {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) lds[lpos(xL(r), LH)] = e[r];
+        __syncthreads();
+#pragma unroll
+        for (int y = 0; y < 8; ++y) gout[(uint32_t)xH(y) + lane_off] = lds[lpos(xH(y), LH)];
+      }
+    } else {
+      if (!COL) {  // ROW inverse: loaded in H pattern, transpose to L through LDS
+#pragma unroll
+        for (int y = 0; y < 8; ++y) lds[lpos(xH(y), LH)] = e[y];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), LH)];
+        __syncthreads();
+      }
+      ntt64_round<2, 0, 2, true, SCALE, PROBE>(a, e, hi, t, false);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) lds[lpos(xL(r), ML)] = e[r];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), ML)];
+      ntt64_round<3, 2, 1, true, SCALE, PROBE>(a, e, hi, t, false);
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), HM)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xH(y), HM)];
+      ntt64_round<3, 5, 0, true, SCALE, PROBE>(a, e, hi, t, COL);
+      if (CANON) {
+#pragma unroll
+        for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
+      }
+#pragma unroll
+      for (int y = 0; y < 8; ++y) gout[((uint32_t)xH(y) << xshift) + lane_off] = e[y];
+    }
+    __syncthreads();  // LDS reuse by the next tile
+  }
+}
+
+#endif  // __HIPCC__
+
+}  // namespace rg

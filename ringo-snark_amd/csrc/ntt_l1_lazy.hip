@@ -1,0 +1,74 @@
+// ntt_l1_lazy.hip -- dispatch of the lazy single-word pass kernels (ntt64.hpp) for the shapes
+// they cover: N = 2^16 as two 8-stage passes, q < 2^63 with q mod 2^32 == 1 (the config-2
+// jindo-modulus prime 47104^4 + 1 and every other p - 1 = b^(2^e) with b even).  Other shapes
+// keep the generic kernels of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r8|r2 forces the generic path.
+#include <cstdlib>
+
+#include "ntt64.hpp"
+#include "ntt_plan.hpp"
+
+namespace rg {
+
+static bool lazy_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RINGO_NTT_KERNEL");
+    v = (e && e[0] == 'r') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+template <bool INV, bool COL, bool SCALE, bool CANON>
+static rg_status launch64(const Ntt64Args& a, hipStream_t st) {
+  const long long tiles = a.total_sub / 16;
+  hipLaunchKernelGGL((ntt64_pass<INV, COL, SCALE, CANON, 1>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+  return check_launch("ntt64_pass");
+}
+
+rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (!p.shoup || p.logN != 16 || p.npasses != 2 || p.passes[0].P != 8 || p.passes[1].P != 8) return RG_OK;
+  const uint64_t q = p.q[0];
+  if ((uint32_t)q != 1u || (q >> 63) != 0 || lazy_disabled()) return RG_OK;
+  *handled = true;
+  const size_t N = (size_t)1 << p.logN;
+  Ntt64Args a{};
+  a.tw = p.tw;
+  a.q = q;
+  a.q2 = 2 * q;
+  a.nqhi = 0u - (uint32_t)(q >> 32);
+  a.ninv = p.nsc[0];
+  a.ninv_p = p.nsc_sh;
+  a.w1n = p.w1n[0];
+  a.w1n_p = p.w1n_sh;
+  a.logN = p.logN;
+  static size_t chunk_polys = 0;
+  if (!chunk_polys) {  // RINGO_NTT_CHUNK_MB bounds the polys per pass pair (default: whole batch)
+    const char* e = getenv("RINGO_NTT_CHUNK_MB");
+    chunk_polys = e ? std::max<size_t>(1, ((size_t)atoi(e) << 20) / (N * 8)) : ~(size_t)0 >> 1;
+  }
+  for (size_t b0 = 0; b0 < p.batch; b0 += chunk_polys) {
+    const size_t nb = std::min(chunk_polys, p.batch - b0);
+    a.total_sub = (long long)(nb * (N >> 8));
+    if (!p.inv) {
+      a.in = p.in + b0 * N;
+      a.out = p.out + b0 * N;
+      a.G0 = 0;
+      RG_TRY((launch64<false, true, false, false>(a, st)));
+      a.in = a.out;
+      a.G0 = 8;
+      RG_TRY((launch64<false, false, false, true>(a, st)));
+    } else {
+      a.in = p.in + b0 * N;
+      a.out = p.out + b0 * N;
+      a.G0 = 8;
+      RG_TRY((launch64<true, false, false, false>(a, st)));
+      a.in = a.out;
+      a.G0 = 0;
+      RG_TRY((launch64<true, true, true, true>(a, st)));
+    }
+  }
+  return RG_OK;
+}
+
+}  // namespace rg

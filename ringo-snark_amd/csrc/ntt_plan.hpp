@@ -27,6 +27,8 @@ struct NttLaunch {
 };
 
 rg_status ntt_run_L1(const NttLaunch& p, hipStream_t st);
+// lazy single-word pass kernels (ntt_l1_lazy.hip); sets *handled when the shape is covered
+rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled);
 rg_status ntt_run_L2(const NttLaunch& p, hipStream_t st);
 rg_status ntt_run_L4(const NttLaunch& p, hipStream_t st);
 rg_status ntt_run_L7(const NttLaunch& p, hipStream_t st);

@@ -21,6 +21,17 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed) {
       if (KIND == 6) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(y[i]));
       if (KIND == 7) asm volatile("v_mul_u32_u24 %0, %1, %0" : "+v"(x[i]) : "v"(a));
       if (KIND == 8) asm volatile("v_mul_f64 %0, %1, %0" : "+v"(f[i]) : "v"((double)a));
+      if (KIND == 9) asm volatile("v_add_co_u32 %0, vcc, %1, %0" : "+v"(x[i]) : "v"(a) : "vcc");
+      if (KIND == 10) asm volatile("v_addc_co_u32 %0, vcc, %1, %0, vcc" : "+v"(x[i]) : "v"(a) : "vcc");
+      if (KIND == 11) asm volatile("v_cndmask_b32 %0, %1, %0, vcc" : "+v"(x[i]) : "v"(a) : "vcc");
+      if (KIND == 12) asm volatile("v_add_co_u32 %0, s[40:41], %1, %0" : "+v"(x[i]) : "v"(a) : "s40", "s41");
+      if (KIND == 13) asm volatile("v_add3_u32 %0, %1, %0, %1" : "+v"(x[i]) : "v"(a));
+      if (KIND == 14) asm volatile("v_cmp_gt_u64 vcc, %0, %1" : : "v"(y[i]), "v"(y[(i + 1) & 7]) : "vcc");
+      if (KIND == 15) asm volatile("v_alignbit_b32 %0, %1, %0, 12" : "+v"(x[i]) : "v"(a));
+      if (KIND == 16) asm volatile("v_mul_hi_u32_u24 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+      if (KIND == 17) asm volatile("v_sub_co_u32 %0, s[40:41], %1, %0\n v_subb_co_u32 %0, s[40:41], %1, %0, s[40:41]" : "+v"(x[i]) : "v"(a) : "s40", "s41");
+      if (KIND == 18) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+      if (KIND == 19) asm volatile("v_cndmask_b32 %0, %1, %0, s[40:41]" : "+v"(x[i]) : "v"(a) : "s40", "s41");
     }
   }
   uint32_t s = 0; for (int i = 0; i < 8; ++i) s += x[i] + (uint32_t)y[i] + (uint32_t)(y[i] >> 32) + (uint32_t)f[i];
@@ -41,5 +52,9 @@ int main() {
   run<0>("v_mad_u64_u32", d, blocks); run<1>("v_mul_hi_u32", d, blocks); run<2>("v_mul_lo_u32", d, blocks);
   run<3>("v_add_u32", d, blocks); run<4>("v_mad_u32_u24", d, blocks); run<5>("v_fma_f64", d, blocks);
   run<6>("v_lshl_add_u64", d, blocks); run<7>("v_mul_u32_u24", d, blocks); run<8>("v_mul_f64", d, blocks);
+  run<9>("v_add_co_u32", d, blocks); run<10>("v_addc_co_u32", d, blocks); run<11>("v_cndmask vcc", d, blocks);
+  run<12>("v_add_co sgpr", d, blocks); run<13>("v_add3_u32", d, blocks); run<14>("v_cmp_gt_u64", d, blocks);
+  run<15>("v_alignbit", d, blocks); run<16>("v_mul_hi_u24", d, blocks); run<17>("sub_co+subb(2)", d, blocks);
+  run<18>("v_pk_add_u16", d, blocks); run<19>("v_cndmask sgpr", d, blocks);
   return 0;
 }
