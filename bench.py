@@ -72,21 +72,24 @@ def parse():
 
 
 class Events:
-    """HIP-event timing of calls on one stream (the stream the kernels are launched on)."""
+    """HIP-event timing of a region on one stream (the stream the kernels are launched on).
+    One event pair brackets the whole timed region: an event between consecutive kernels makes
+    the runtime insert a release fence that writes back the caches, which perturbs what is
+    measured (tools/nttlab/pass_lab: ~15-25% slower with per-pass events)."""
 
     def __init__(self, torch, stream):
-        self.torch, self.stream, self.pairs = torch, stream, []
+        self.torch, self.stream = torch, stream
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e1 = torch.cuda.Event(enable_timing=True)
 
-    def time(self, fn):
-        e0 = self.torch.cuda.Event(enable_timing=True)
-        e1 = self.torch.cuda.Event(enable_timing=True)
-        e0.record(self.stream)
-        fn()
-        e1.record(self.stream)
-        self.pairs.append((e0, e1))
+    def start(self):
+        self.e0.record(self.stream)
+
+    def stop(self):
+        self.e1.record(self.stream)
 
     def total_ms(self):
-        return sum(a.elapsed_time(b) for a, b in self.pairs)
+        return self.e0.elapsed_time(self.e1)
 
 
 def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
@@ -99,13 +102,9 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     ref = x.clone()
     stream = torch.cuda.current_stream()
 
-    def step(ev=None):
-        if ev is None:
-            T.fwd_dev(x, x, batch, stream)
-            T.inv_dev(x, x, batch, stream)
-        else:
-            ev.time(lambda: T.fwd_dev(x, x, batch, stream))
-            ev.time(lambda: T.inv_dev(x, x, batch, stream))
+    def step():
+        T.fwd_dev(x, x, batch, stream)
+        T.inv_dev(x, x, batch, stream)
 
     for _ in range(warmup):
         step()
@@ -115,8 +114,10 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     torch.cuda.synchronize()
     ev = Events(torch, stream)
     t0 = time.perf_counter()
+    ev.start()
     for _ in range(steps):
-        step(ev)
+        step()
+    ev.stop()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -176,8 +177,10 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world)
         dist.barrier()
     ev = Events(torch, stream)
     t0 = time.perf_counter()
+    ev.start()
     for _ in range(steps):
-        ev.time(step)
+        step()
+    ev.stop()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -261,7 +264,7 @@ def main():
                    "rank": N, "field_bits": 63, "batch_per_gpu": args.batch, "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "NTT transform = 2 LDS-tiled pass kernels (ntt_pass_kernel<1,8,..>) per chunk",
+                     "kernel": "NTT transform = ntt16_pass COL + ROW (2 launches per transform batch); region time / transforms",
                      "bytes_per_unit": bytes_per_ntt},
         "selfcheck_fwd_inv_identity": ok,
     }

@@ -215,34 +215,56 @@ struct Ntt64Args {
   int logN, G0;
 };
 
+// ----------------------------------------------------------------------------------------
+// N = 2^16 specialisation: compile-time strides, buffer addressing (one VGPR offset per access
+// pattern, per-access constants in SGPR soffsets / immediates) and one tile per workgroup, so
+// no address is held in registers across the tile.  COL = global stages [0, 8) on the 256
+// columns (stride 256), ROW = [8, 16) on the 256 rows.  Patterns and index algebra as above.
+// ----------------------------------------------------------------------------------------
+typedef unsigned int rg_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int rg_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_buf(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ uint64_t rg_bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const rg_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return pk(v.x, v.y);
+}
+__device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  rg_u32x2 v;
+  v.x = lo32(x);
+  v.y = hi32(x);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
+}
+
 // PROBE (tuning only; production = 0): 1 = twiddles from registers (no table loads),
-// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both
-template <int RK, int LO, int PAT, bool INV, bool SCALE, int PROBE = 0>
-__device__ __forceinline__ void ntt64_round(const Ntt64Args& a, uint64_t (&e)[8], long long hi, int t, bool uniform) {
-  // pat: 0 = H, 1 = M, 2 = L.  x(rho) for register rho of this thread:
-  auto xof = [&](int rho) -> int {
-    if (PAT == 0) return t + 32 * rho;
-    if (PAT == 1) return ((t >> 2) << 5) | (rho << 2) | (t & 3);
-    return 8 * t + rho;
+// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both,
+// 16 = at most two butterflies in flight (register pressure)
+template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, int PROBE>
+__device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
+                                            uint32_t hi, uint32_t t) {
+  constexpr int G0 = COL ? 0 : 8;
+  constexpr bool UNIFORM = COL && PAT == 0;  // twiddle index independent of the lane
+  auto xof = [&](int rho) -> uint32_t {
+    if (PAT == 0) return t + 32u * rho;
+    if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
+    return 8u * t + rho;
   };
-  constexpr int NPK = 1 << RK;  // points per group
+  constexpr int NPK = 1 << RK;
 #pragma unroll
   for (int sp = 0; sp < RK; ++sp) {
-    // forward: window bits processed top-down; inverse: bottom-up
-    const int bw = INV ? sp : (RK - 1 - sp);  // bit within the window
-    const int b = LO + bw;                     // bit of x
-    const int k = 7 - b;                       // local stage
+    const int bw = INV ? sp : (RK - 1 - sp);
+    const int b = LO + bw;
+    const int k = 7 - b;
     const int half = 1 << bw;
-    const bool last = INV && SCALE && k == 0;  // SCALE: this pass holds global stage 0
+    const bool last = INV && SCALE && k == 0;
     uint64_t w[4], wp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      // j-th pair: rho0 has bit bw clear
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
-      // pairs that share x >> (b+1) reuse the twiddle of the previous pair
-      const int hb = (jj & (half - 1)) != 0;
-      if (hb) {
+      if ((jj & (half - 1)) != 0) {
         w[j] = w[j - 1];
         wp[j] = wp[j - 1];
         continue;
@@ -252,22 +274,30 @@ __device__ __forceinline__ void ntt64_round(const Ntt64Args& a, uint64_t (&e)[8]
         wp[j] = a.w1n_p;
         continue;
       }
-      long long idx = (1LL << (a.G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
-      if (uniform) idx = __builtin_amdgcn_readfirstlane((int)idx);
-      if constexpr (PROBE & 1) {
-        w[j] = a.w1n + (uint64_t)idx;
+      if constexpr ((PROBE & 1) != 0) {
+        w[j] = a.w1n + (xof(rho0) >> (b + 1)) + hi;
         wp[j] = a.w1n_p;
-        continue;
+      } else if constexpr (UNIFORM) {
+        const uint32_t idx = (1u << (G0 + k)) + (xof(rho0) >> (b + 1));
+        const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[iu];
+        w[j] = v.x;
+        wp[j] = v.y;
+      } else {
+        const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
+        const rg_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(twr, idx * 16u, 0, 0);
+        w[j] = pk(v.x, v.y);
+        wp[j] = pk(v.z, v.w);
       }
-      const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[idx];
-      w[j] = v.x;
-      wp[j] = v.y;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
       const int rho1 = rho0 + half;
+      if constexpr ((PROBE & 16) != 0) {
+        if ((j & 1) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
       if constexpr ((PROBE & 2) != 0) {
         e[rho0] += e[rho1] ^ w[j] ^ wp[j];
       } else if constexpr (!INV) {
@@ -280,100 +310,155 @@ __device__ __forceinline__ void ntt64_round(const Ntt64Args& a, uint64_t (&e)[8]
   }
 }
 
-// CANON: map the outputs to [0, q) (last pass of a transform); SCALE: inverse with the fused
-// N^-1 (COL pass of the inverse, global stage 0 inside)
-template <bool INV, bool COL, bool SCALE, bool CANON, int MINW, int PROBE = 0>
-__global__ __launch_bounds__(512, MINW) void ntt64_pass(Ntt64Args a) {
-  constexpr int SW = 16, PADN = 288;
-  __shared__ uint64_t lds[SW * PADN];
-  const int tid = threadIdx.x;
-  const int s = COL ? (tid & 15) : (tid >> 5);
-  const int t = COL ? (tid >> 4) : (tid & 31);
-  const int logS = a.logN - a.G0 - 8;
-  const int rowshift = a.logN - a.G0;
-  const long long ntiles = a.total_sub / SW;
-  const uint32_t lane_off = COL ? (uint32_t)s : ((uint32_t)s << rowshift);
-  const int xshift = COL ? logS : 0;
-  // LDS images: COL: transposed [x][s], 16 x + s + 16 (x >> 3); ROW: [s][x] + per-exchange pad
-  enum { HM, ML, LH };
-  auto lpos = [&](int x, int ph) {
-    if (COL) return 16 * x + s + 16 * (x >> 3);
-    return s * PADN + x + (ph == HM ? 4 * (x >> 5) : ph == ML ? (x >> 3) : (x >> 5));
-  };
-  auto xH = [&](int y) { return t + 32 * y; };
-  auto xM = [&](int y) { return ((t >> 2) << 5) | (y << 2) | (t & 3); };
-  auto xL = [&](int r) { return 8 * t + r; };
-  constexpr bool LOAD_L = INV && COL;  // inverse COL starts in the L pattern
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const long long sub0 = tile * SW;
-    const long long base = COL ? (((sub0 >> logS) << rowshift) + (sub0 & ((1LL << logS) - 1))) : (sub0 << rowshift);
-    const uint64_t* gin = a.in + base;
-    uint64_t* gout = a.out + base;
-    const long long hi = COL ? 0 : ((sub0 + s) & ((1LL << a.G0) - 1));
-    uint64_t e[8];
+template <bool INV, bool COL, bool SCALE, bool CANON, int MINW = 1, int PROBE = 0>
+__global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
+  __shared__ uint64_t lds[16 * 288];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
+  const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
+  const uint32_t tile = blockIdx.x;
+  // tile base (elements): COL: poly * 2^16 + column block * 16; ROW: 16 rows of 256
+  const size_t tbase = COL ? (((size_t)(tile >> 4) << 16) + ((tile & 15u) << 4)) : ((size_t)tile << 12);
+  const __amdgpu_buffer_rsrc_t rin = rg_buf(a.in + tbase);
+  const __amdgpu_buffer_rsrc_t rout = rg_buf(a.out + tbase);
+  const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
+  const uint32_t hi = COL ? 0u : (((tile << 4) + s) & 255u);
+  // per-pattern LDS bases (u64 index) -- see the layout derivation in DESIGN.md
+  uint32_t bH, bM, bL;  // exchange-dependent for ROW
+  uint64_t e[8];
+  // ---- global load
+  if constexpr (COL) {
+    if constexpr (!INV) {
+      const uint32_t vo = ((t << 8) + s) * 8u;
 #pragma unroll
-    for (int y = 0; y < 8; ++y) e[y] = gin[((uint32_t)(LOAD_L ? xL(y) : xH(y)) << xshift) + lane_off];
-    if (!INV) {
-      ntt64_round<3, 5, 0, false, false, PROBE>(a, e, hi, t, COL);
-#pragma unroll
-      for (int y = 0; y < 8; ++y) lds[lpos(xH(y), HM)] = e[y];
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), HM)];
-      ntt64_round<3, 2, 1, false, false, PROBE>(a, e, hi, t, false);
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), ML)] = e[y];
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), ML)];
-      ntt64_round<2, 0, 2, false, false, PROBE>(a, e, hi, t, false);
-      if (CANON) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
-      }
-      if (COL) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) gout[((uint32_t)xL(r) << xshift) + lane_off] = e[r];
-      } else {
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) lds[lpos(xL(r), LH)] = e[r];
-        __syncthreads();
-#pragma unroll
-        for (int y = 0; y < 8; ++y) gout[(uint32_t)xH(y) + lane_off] = lds[lpos(xH(y), LH)];
-      }
+      for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo, (uint32_t)y << 16);
     } else {
-      if (!COL) {  // ROW inverse: loaded in H pattern, transpose to L through LDS
+      const uint32_t vo = ((t << 11) + s) * 8u;
 #pragma unroll
-        for (int y = 0; y < 8; ++y) lds[lpos(xH(y), LH)] = e[y];
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) e[r] = lds[lpos(xL(r), LH)];
-        __syncthreads();
-      }
-      ntt64_round<2, 0, 2, true, SCALE, PROBE>(a, e, hi, t, false);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) lds[lpos(xL(r), ML)] = e[r];
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xM(y), ML)];
-      ntt64_round<3, 2, 1, true, SCALE, PROBE>(a, e, hi, t, false);
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) lds[lpos(xM(y), HM)] = e[y];
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[lpos(xH(y), HM)];
-      ntt64_round<3, 5, 0, true, SCALE, PROBE>(a, e, hi, t, COL);
-      if (CANON) {
-#pragma unroll
-        for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
-      }
-#pragma unroll
-      for (int y = 0; y < 8; ++y) gout[((uint32_t)xH(y) << xshift) + lane_off] = e[y];
+      for (int r = 0; r < 8; ++r) e[r] = rg_bload(rin, vo, (uint32_t)r << 11);
     }
-    __syncthreads();  // LDS reuse by the next tile
+  } else {
+    const uint32_t vo = ((s << 8) + t) * 8u;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
+  }
+  if constexpr (COL) {
+    bH = 16 * t + s + 16 * (t >> 3);
+    bM = s + 16 * (t & 3) + 576 * (t >> 2);
+    bL = 144 * t + s;
+  }
+  auto offH = [&](int y) { return COL ? 576 * y : 0; };
+  auto offM = [&](int y) { return COL ? 64 * y + 16 * (y >> 1) : 0; };
+  if constexpr (!INV) {
+    ntt16_round<3, 5, 0, false, false, COL, PROBE>(a, twr, e, hi, t);
+    // exchange H -> M
+    if constexpr (COL) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[bH + offH(y)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[bM + offM(y)];
+    } else {  // pad 4 (x >> 5)
+      const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[h + 36 * y] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[m + 4 * y];
+    }
+    ntt16_round<3, 2, 1, false, false, COL, PROBE>(a, twr, e, hi, t);
+    __syncthreads();
+    // exchange M -> L
+    if constexpr (COL) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[bM + offM(y)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[bL + 16 * r];
+    } else {  // pad (x >> 3)
+      const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[m + 4 * y + (y >> 1)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[l + r];
+    }
+    ntt16_round<2, 0, 2, false, false, COL, PROBE>(a, twr, e, hi, t);
+    if (CANON) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
+    }
+    if constexpr (COL) {
+      const uint32_t vo = ((t << 11) + s) * 8u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) rg_bstore(e[r], rout, vo, (uint32_t)r << 11);
+    } else {  // L -> H through LDS (pad x >> 5), then coalesced rows
+      const uint32_t l = 288 * s + 8 * t + (t >> 2), h = 288 * s + t;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) lds[l + r] = e[r];
+      __syncthreads();
+      const uint32_t vo = ((s << 8) + t) * 8u;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) rg_bstore(lds[h + 33 * y], rout, vo + 256u * y, 0);
+    }
+  } else {
+    if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
+      const uint32_t h = 288 * s + t, l = 288 * s + 8 * t + (t >> 2);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[h + 33 * y] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[l + r];
+      __syncthreads();
+    }
+    ntt16_round<2, 0, 2, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    // exchange L -> M
+    if constexpr (COL) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) lds[bL + 16 * r] = e[r];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[bM + offM(y)];
+    } else {  // pad x >> 3
+      const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) lds[l + r] = e[r];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[m + 4 * y + (y >> 1)];
+    }
+    ntt16_round<3, 2, 1, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    __syncthreads();
+    // exchange M -> H
+    if constexpr (COL) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[bM + offM(y)] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[bH + offH(y)];
+    } else {  // pad 4 (x >> 5)
+      const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
+#pragma unroll
+      for (int y = 0; y < 8; ++y) lds[m + 4 * y] = e[y];
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[h + 36 * y];
+    }
+    ntt16_round<3, 5, 0, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    if (CANON) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
+    }
+    if constexpr (COL) {
+      const uint32_t vo = ((t << 8) + s) * 8u;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo, (uint32_t)y << 16);
+    } else {
+      const uint32_t vo = ((s << 8) + t) * 8u;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo + 256u * y, 0);
+    }
   }
 }
 

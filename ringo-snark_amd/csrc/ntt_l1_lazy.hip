@@ -21,8 +21,8 @@ static bool lazy_disabled() {
 template <bool INV, bool COL, bool SCALE, bool CANON>
 static rg_status launch64(const Ntt64Args& a, hipStream_t st) {
   const long long tiles = a.total_sub / 16;
-  hipLaunchKernelGGL((ntt64_pass<INV, COL, SCALE, CANON, 1>), dim3((unsigned)tiles), dim3(512), 0, st, a);
-  return check_launch("ntt64_pass");
+  hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+  return check_launch("ntt16_pass");
 }
 
 rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled) {

@@ -40,7 +40,8 @@ static uint64_t powmod(uint64_t a, uint64_t e, uint64_t q) {
 
 template <bool INV, bool COL, bool SCALE, bool CANON, int MINW, int PROBE>
 static void launch(const Ntt64Args& a, int grid) {
-  hipLaunchKernelGGL((ntt64_pass<INV, COL, SCALE, CANON, MINW, PROBE>), dim3(grid), dim3(512), 0, 0, a);
+  (void)grid;
+  hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, MINW, (PROBE & 255)>), dim3((unsigned)(a.total_sub / 16)), dim3(512), 0, 0, a);
 }
 
 template <int MINW, int PROBE = 0>
@@ -113,7 +114,7 @@ static void run_variant(const char* name, Ntt64Args base, const uint64_t* d_tw, 
 }
 
 // fwd+inv over the whole batch in chunks of `chunk` polys (col+row per chunk), full kernels
-template <int PROBE = 0>
+template <int PROBE = 0, int MINW = 1>
 static void run_chunked(const char* name, Ntt64Args base, const uint64_t* d_tw, const uint64_t* d_twi, uint64_t* d_x,
                         size_t batch, int N, size_t chunk) {
   Ntt64Args f = base, r = base;
@@ -126,8 +127,8 @@ static void run_chunked(const char* name, Ntt64Args base, const uint64_t* d_tw, 
       const int grid = (int)(tsub / 16);
       f.in = f.out = d_x + b0 * N;
       f.total_sub = tsub;
-      f.G0 = 0; launch<false, true, false, false, 1, PROBE>(f, grid);
-      f.G0 = 8; launch<false, false, false, true, 1, PROBE>(f, grid);
+      f.G0 = 0; launch<false, true, false, false, MINW, PROBE>(f, grid);
+      f.G0 = 8; launch<false, false, false, true, MINW, PROBE>(f, grid);
     }
     for (size_t b0 = 0; b0 < batch; b0 += chunk) {
       const size_t nb = std::min(chunk, batch - b0);
@@ -135,8 +136,8 @@ static void run_chunked(const char* name, Ntt64Args base, const uint64_t* d_tw, 
       const int grid = (int)(tsub / 16);
       r.in = r.out = d_x + b0 * N;
       r.total_sub = tsub;
-      r.G0 = 8; launch<true, false, false, false, 1, PROBE>(r, grid);
-      r.G0 = 0; launch<true, true, true, true, 1, PROBE>(r, grid);
+      r.G0 = 8; launch<true, false, false, false, MINW, PROBE>(r, grid);
+      r.G0 = 0; launch<true, true, true, true, MINW, PROBE>(r, grid);
     }
   };
   step();
@@ -206,13 +207,12 @@ int main(int argc, char** argv) {
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   (void)cus;
-  for (size_t ch : {16, 32, 48, 64, 96, 128, 192, 1024}) run_chunked("chunked full", base, d_tw, d_twi, d_x, batch, N, ch);
-  for (size_t ch : {16, 32, 64, 128, 1024}) run_chunked<3>("chunked probe:neither", base, d_tw, d_twi, d_x, batch, N, ch);
-  for (int rep = 0; rep < 1; ++rep) {
-    run_variant<1>("ntt64 full", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
-    run_variant<1, 1>("probe: no tw loads", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
-    run_variant<1, 2>("probe: no bfly arith", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
-    run_variant<1, 3>("probe: neither", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
+  for (int rep = 0; rep < 2; ++rep) {
+    run_chunked<256>("ntt16", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 1>("ntt16 probe no-tw", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 2>("ntt16 probe no-arith", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 3>("ntt16 probe neither", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
   }
+  run_variant<1, 256>("ntt16 (per-pass events)", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
   return 0;
 }
