@@ -310,13 +310,16 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
   }
 }
 
-template <bool INV, bool COL, bool SCALE, bool CANON, int MINW = 1, int PROBE = 0>
-__global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
-  __shared__ uint64_t lds[16 * 288];
+// PROBE & 32: keep every LDS access a single ds_*_b64 (no ds_*2 merging) -- bank-conflict study
+#define RG_NM() \
+  do {                                            \
+    if constexpr ((PROBE & 32) != 0) asm volatile("" ::: "memory"); \
+  } while (0)
+template <bool INV, bool COL, bool SCALE, bool CANON, int PROBE = 0>
+__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds) {
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
-  const uint32_t tile = blockIdx.x;
   // tile base (elements): COL: poly * 2^16 + column block * 16; ROW: 16 rows of 256
   const size_t tbase = COL ? (((size_t)(tile >> 4) << 16) + ((tile & 15u) << 4)) : ((size_t)tile << 12);
   const __amdgpu_buffer_rsrc_t rin = rg_buf(a.in + tbase);
@@ -361,10 +364,16 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
     } else {  // pad 4 (x >> 5)
       const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[h + 36 * y] = e[y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        lds[h + 36 * y] = e[y];
+      }
       __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[m + 4 * y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        e[y] = lds[m + 4 * y];
+      }
     }
     ntt16_round<3, 2, 1, false, false, COL, PROBE>(a, twr, e, hi, t);
     __syncthreads();
@@ -378,10 +387,16 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
     } else {  // pad (x >> 3)
       const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[m + 4 * y + (y >> 1)] = e[y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        lds[m + 4 * y + (y >> 1)] = e[y];
+      }
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) e[r] = lds[l + r];
+      for (int r = 0; r < 8; ++r) {
+        RG_NM();
+        e[r] = lds[l + r];
+      }
     }
     ntt16_round<2, 0, 2, false, false, COL, PROBE>(a, twr, e, hi, t);
     if (CANON) {
@@ -396,20 +411,32 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
       const uint32_t l = 288 * s + 8 * t + (t >> 2), h = 288 * s + t;
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) lds[l + r] = e[r];
+      for (int r = 0; r < 8; ++r) {
+        RG_NM();
+        lds[l + r] = e[r];
+      }
       __syncthreads();
       const uint32_t vo = ((s << 8) + t) * 8u;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) rg_bstore(lds[h + 33 * y], rout, vo + 256u * y, 0);
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        rg_bstore(lds[h + 33 * y], rout, vo + 256u * y, 0);
+      }
     }
   } else {
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
       const uint32_t h = 288 * s + t, l = 288 * s + 8 * t + (t >> 2);
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[h + 33 * y] = e[y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        lds[h + 33 * y] = e[y];
+      }
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) e[r] = lds[l + r];
+      for (int r = 0; r < 8; ++r) {
+        RG_NM();
+        e[r] = lds[l + r];
+      }
       __syncthreads();
     }
     ntt16_round<2, 0, 2, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
@@ -423,10 +450,16 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
     } else {  // pad x >> 3
       const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) lds[l + r] = e[r];
+      for (int r = 0; r < 8; ++r) {
+        RG_NM();
+        lds[l + r] = e[r];
+      }
       __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[m + 4 * y + (y >> 1)];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        e[y] = lds[m + 4 * y + (y >> 1)];
+      }
     }
     ntt16_round<3, 2, 1, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
     __syncthreads();
@@ -440,10 +473,16 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
     } else {  // pad 4 (x >> 5)
       const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[m + 4 * y] = e[y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        lds[m + 4 * y] = e[y];
+      }
       __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[h + 36 * y];
+      for (int y = 0; y < 8; ++y) {
+        RG_NM();
+        e[y] = lds[h + 36 * y];
+      }
     }
     ntt16_round<3, 5, 0, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
     if (CANON) {
@@ -459,6 +498,47 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
 #pragma unroll
       for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo + 256u * y, 0);
     }
+  }
+}
+
+
+template <bool INV, bool COL, bool SCALE, bool CANON, int MINW = 1, int PROBE = 0>
+__global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
+  __shared__ uint64_t lds[16 * 288];
+  ntt16_tile<INV, COL, SCALE, CANON, PROBE>(a, blockIdx.x, lds);
+}
+
+// Software-pipelined pair of passes over consecutive chunks of polynomials: one launch runs the
+// second pass of chunk k-1 (args b, nb tiles) together with the first pass of chunk k (args f,
+// nf tiles), interleaved tile by tile.  Chunk k-1's pass-1 output was written by the previous
+// launch moments earlier and is re-read from the 256 MiB Infinity Cache, and the in-place
+// pass-2 output overwrites those same (still cached) lines, so HBM sees about one read and one
+// write per transform instead of two of each.
+//   forward: pass 1 = COL, pass 2 = ROW (+ canonical output);  inverse: pass 1 = ROW,
+//   pass 2 = COL (+ N^-1 and canonical output)
+template <bool INV, int MINW = 1, int PROBE = 0>
+__global__ __launch_bounds__(512, MINW) void ntt16_pipe(Ntt64Args f, uint32_t nf, Ntt64Args b, uint32_t nb) {
+  __shared__ uint64_t lds[16 * 288];
+  const uint32_t i = blockIdx.x, m = nf < nb ? nf : nb;
+  uint32_t tb, tf;
+  bool second;
+  if (i < 2 * m) {
+    second = (i & 1) == 0;
+    tb = tf = i >> 1;
+  } else {
+    second = nb > nf;
+    tb = tf = i - m;
+  }
+  if (second) {
+    if constexpr (!INV)
+      ntt16_tile<false, false, false, true, PROBE>(b, tb, lds);
+    else
+      ntt16_tile<true, true, true, true, PROBE>(b, tb, lds);
+  } else {
+    if constexpr (!INV)
+      ntt16_tile<false, true, false, false, PROBE>(f, tf, lds);
+    else
+      ntt16_tile<true, false, false, false, PROBE>(f, tf, lds);
   }
 }
 

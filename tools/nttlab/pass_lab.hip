@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/ringo.h"
@@ -26,6 +27,26 @@ using namespace rg;
       exit(1);                                                        \
     }                                                                 \
   } while (0)
+
+
+// min and median over `reps` timed repetitions of fn (one event pair per repetition)
+template <class F>
+static void time_reps(F fn, int reps, float& tmin, float& tmed) {
+  std::vector<float> v;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  fn();
+  for (int k = 0; k < reps; ++k) {
+    CK(hipEventRecord(a));
+    fn();
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    v.push_back(ms);
+  }
+  std::sort(v.begin(), v.end());
+  tmin = v[0];
+  tmed = v[v.size() / 2];
+}
 
 static uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) { return (unsigned __int128)a * b % q; }
 static uint64_t powmod(uint64_t a, uint64_t e, uint64_t q) {
@@ -140,16 +161,63 @@ static void run_chunked(const char* name, Ntt64Args base, const uint64_t* d_tw, 
       r.G0 = 0; launch<true, true, true, true, MINW, PROBE>(r, grid);
     }
   };
-  step();
-  hipEvent_t a, b;
-  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-  const int reps = 5;
-  CK(hipEventRecord(a));
-  for (int k = 0; k < reps; ++k) step();
-  CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
-  float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= reps;
-  printf("%-26s chunk %4zu  fwd+inv %8.1f us | %.3f M NTT/s (%.1f%% HBM)\n", name, chunk, ms * 1e3,
-         2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12);
+  float ms, med;
+  time_reps(step, 8, ms, med);
+  printf("%-26s chunk %4zu  fwd+inv min %7.1f med %7.1f us | %.3f M NTT/s (%.1f%% HBM)\n", name, chunk, ms * 1e3,
+         med * 1e3, 2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12);
+}
+
+// pipelined chunks: launch k = pass 2 of chunk k-1 + pass 1 of chunk k
+template <int PROBE = 0>
+static void run_pipe(const char* name, Ntt64Args base, const uint64_t* d_tw, const uint64_t* d_twi, uint64_t* d_x,
+                     const uint64_t* d_src, const uint64_t* d_ref, size_t batch, int N, size_t chunk) {
+  const size_t nch = (batch + chunk - 1) / chunk;
+  auto args = [&](size_t c, const uint64_t* tw, uint32_t& ntiles) {
+    Ntt64Args a = base;
+    a.tw = tw;
+    const size_t b0 = c * chunk, nb = std::min(chunk, batch - b0);
+    a.in = a.out = d_x + b0 * N;
+    a.total_sub = (long long)nb * (N >> 8);
+    ntiles = (uint32_t)(a.total_sub / 16);
+    return a;
+  };
+  auto fwd = [&]() {
+    for (size_t k = 0; k <= nch; ++k) {
+      uint32_t nf = 0, nb = 0;
+      Ntt64Args f = base, b = base;
+      if (k < nch) { f = args(k, d_tw, nf); f.G0 = 0; }
+      if (k > 0) { b = args(k - 1, d_tw, nb); b.G0 = 8; }
+      hipLaunchKernelGGL((ntt16_pipe<false, 1, PROBE>), dim3(nf + nb), dim3(512), 0, 0, f, nf, b, nb);
+    }
+  };
+  auto inv = [&]() {
+    for (size_t k = 0; k <= nch; ++k) {
+      uint32_t nf = 0, nb = 0;
+      Ntt64Args f = base, b = base;
+      if (k < nch) { f = args(k, d_twi, nf); f.G0 = 8; }
+      if (k > 0) { b = args(k - 1, d_twi, nb); b.G0 = 0; }
+      hipLaunchKernelGGL((ntt16_pipe<true, 1, PROBE>), dim3(nf + nb), dim3(512), 0, 0, f, nf, b, nb);
+    }
+  };
+  const size_t bytes = batch * N * 8;
+  CK(hipMemcpy(d_x, d_src, bytes, hipMemcpyDeviceToDevice));
+  fwd();
+  CK(hipDeviceSynchronize());
+  std::vector<uint64_t> got(batch * N), want(batch * N), src(batch * N);
+  CK(hipMemcpy(got.data(), d_x, bytes, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(want.data(), d_ref, bytes, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(src.data(), d_src, bytes, hipMemcpyDeviceToHost));
+  size_t badf = 0, badi = 0;
+  for (size_t i = 0; i < got.size(); ++i) badf += got[i] != want[i];
+  inv();
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(got.data(), d_x, bytes, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < got.size(); ++i) badi += got[i] != src[i];
+  float ms, med;
+  time_reps([&]() { fwd(); inv(); }, 8, ms, med);
+  printf("%-26s chunk %4zu  fwd+inv min %7.1f med %7.1f us | %.3f M NTT/s (%.1f%% HBM)  fwd %s inv %s\n", name, chunk, ms * 1e3, med * 1e3,
+         2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12,
+         badf ? "MISMATCH" : "ok", badi ? "MISMATCH" : "ok");
 }
 
 int main(int argc, char** argv) {
@@ -195,11 +263,22 @@ int main(int argc, char** argv) {
   {
     CK(hipMemcpy(d_x, d_src, bytes, hipMemcpyDeviceToDevice));
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-    float ms; const int reps = 5;
-    CK(hipEventRecord(a));
-    for (int k = 0; k < reps; ++k) { RK(rg_ntt_fwd_dev(T, d_x, d_x, batch, nullptr)); RK(rg_ntt_inv_dev(T, d_x, d_x, batch, nullptr)); }
-    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
-    ms /= reps;
+    float ms, med;
+    // clock ramp: per-repetition times of the first 40 production steps
+    {
+      hipEvent_t c0, c1;
+      CK(hipEventCreate(&c0)); CK(hipEventCreate(&c1));
+      printf("ramp (us):");
+      for (int k = 0; k < 40; ++k) {
+        CK(hipEventRecord(c0));
+        RK(rg_ntt_fwd_dev(T, d_x, d_x, batch, nullptr)); RK(rg_ntt_inv_dev(T, d_x, d_x, batch, nullptr));
+        CK(hipEventRecord(c1)); CK(hipEventSynchronize(c1));
+        float t; CK(hipEventElapsedTime(&t, c0, c1));
+        printf(" %.0f", t * 1e3);
+      }
+      printf("\n");
+    }
+    time_reps([&]() { RK(rg_ntt_fwd_dev(T, d_x, d_x, batch, nullptr)); RK(rg_ntt_inv_dev(T, d_x, d_x, batch, nullptr)); }, 8, ms, med);
     printf("%-26s fwd+inv %.1f us  | %.3f M NTT/s (%.1f%% HBM)\n", "libringo (production)", ms * 1e3,
            2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12);
   }
@@ -207,12 +286,11 @@ int main(int argc, char** argv) {
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   (void)cus;
-  for (int rep = 0; rep < 2; ++rep) {
+  for (int rep = 0; rep < 3; ++rep) {
     run_chunked<256>("ntt16", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
-    run_chunked<256 + 1>("ntt16 probe no-tw", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
-    run_chunked<256 + 2>("ntt16 probe no-arith", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
-    run_chunked<256 + 3>("ntt16 probe neither", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 32>("ntt16 no-ds-merge", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
   }
-  run_variant<1, 256>("ntt16 (per-pass events)", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
+  run_variant<1, 256>("ntt16 per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
+  run_variant<1, 256 + 32>("ntt16 no-ds-merge per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
   return 0;
 }
