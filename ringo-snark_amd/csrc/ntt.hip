@@ -162,6 +162,27 @@ static rg_status finalize(rg_ntt* t) {
       b[2 * i] = wi;
       b[2 * i + 1] = h_shoup(wi, q);
     }
+    if (t->logN == 16) {  // lane-ordered ROW last-round copy for ntt16_pass (ntt64.hpp)
+      auto add_row_copy = [&](std::vector<uint64_t>& v) {
+        const size_t base = v.size();
+        v.resize(base + (size_t)2 * 256 * 192);
+        for (int r = 0; r < 256; ++r)
+          for (int tt = 0; tt < 32; ++tt) {
+            for (int g = 0; g < 2; ++g) {
+              const size_t src = (size_t)(1 << 14) + 64 * r + 2 * tt + g, dst = (size_t)r * 192 + 32 * g + tt;
+              v[base + 2 * dst] = v[2 * src];
+              v[base + 2 * dst + 1] = v[2 * src + 1];
+            }
+            for (int j = 0; j < 4; ++j) {
+              const size_t src = (size_t)(1 << 15) + 128 * r + 4 * tt + j, dst = (size_t)r * 192 + 64 + 32 * j + tt;
+              v[base + 2 * dst] = v[2 * src];
+              v[base + 2 * dst + 1] = v[2 * src + 1];
+            }
+          }
+      };
+      add_row_copy(a);
+      add_row_copy(b);
+    }
     RG_TRY(t->d_tw.upload(a.data(), a.size() * 8));
     RG_TRY(t->d_twinv.upload(b.data(), b.size() * 8));
     uint64_t nv, wv;

@@ -206,7 +206,11 @@ __device__ __forceinline__ uint64_t canon_x(uint64_t x, uint64_t q) {
 struct Ntt64Args {
   const uint64_t* in;
   uint64_t* out;
-  const uint64_t* tw;  // (w, floor(w 2^64 / q)) pairs, forward or inverse table, [N][2]
+  // (w, floor(w 2^64 / q)) pairs, forward or inverse: [N] in the reference order tw[m + i]
+  // (ntt.go:153-203), then for N = 2^16 a lane-ordered copy of the ROW pass's last two stages:
+  // row r, stage 14: [r*192 + 32 g + t] = tw[2^14 + 64 r + 2 t + g]       (g < 2,  t < 32)
+  //        stage 15: [r*192 + 64 + 32 j + t] = tw[2^15 + 128 r + 4 t + j] (j < 4)
+  const uint64_t* tw;
   uint64_t q, q2;
   uint32_t nqhi, pad_;
   uint64_t ninv, ninv_p;  // N^-1 and its Shoup quotient (inverse, last stage)
@@ -216,10 +220,15 @@ struct Ntt64Args {
 };
 
 // ----------------------------------------------------------------------------------------
-// N = 2^16 specialisation: compile-time strides, buffer addressing (one VGPR offset per access
+// N = 2^16 pass kernel: compile-time strides, buffer addressing (one VGPR offset per access
 // pattern, per-access constants in SGPR soffsets / immediates) and one tile per workgroup, so
 // no address is held in registers across the tile.  COL = global stages [0, 8) on the 256
-// columns (stride 256), ROW = [8, 16) on the 256 rows.  Patterns and index algebra as above.
+// columns (stride 256), ROW = [8, 16) on the 256 rows.
+// Tiles: COL = 16 adjacent columns of one polynomial.  ROW = 16 rows; with RP ("row-major over
+// polynomials", batch % 16 == 0) the 16 rows are the SAME row of 16 consecutive polynomials,
+// so every twiddle of the tile is shared by all 16 sub-transforms (as in COL): the first
+// round's twiddles come from scalar loads and the others are loaded once per lane slot t,
+// shared by both half-waves.  Without RP the 16 rows are 16 consecutive rows of one poly.
 // ----------------------------------------------------------------------------------------
 typedef unsigned int rg_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int rg_u32x4 __attribute__((ext_vector_type(4)));
@@ -239,13 +248,12 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 }
 
 // PROBE (tuning only; production = 0): 1 = twiddles from registers (no table loads),
-// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both,
-// 16 = at most two butterflies in flight (register pressure)
-template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, int PROBE>
+// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both
+template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
                                             uint32_t hi, uint32_t t) {
   constexpr int G0 = COL ? 0 : 8;
-  constexpr bool UNIFORM = COL && PAT == 0;  // twiddle index independent of the lane
+  constexpr bool UNIFORM = (COL || RP) && PAT == 0;  // twiddle index independent of the lane
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
@@ -258,13 +266,13 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
     const int b = LO + bw;
     const int k = 7 - b;
     const int half = 1 << bw;
-    const bool last = INV && SCALE && k == 0;
+    const bool last = INV && SCALE && k == 0;  // SCALE: this pass holds global stage 0
     uint64_t w[4], wp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
-      if ((jj & (half - 1)) != 0) {
+      if ((jj & (half - 1)) != 0) {  // same x >> (b+1) as the previous pair
         w[j] = w[j - 1];
         wp[j] = wp[j - 1];
         continue;
@@ -278,11 +286,18 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
         w[j] = a.w1n + (xof(rho0) >> (b + 1)) + hi;
         wp[j] = a.w1n_p;
       } else if constexpr (UNIFORM) {
-        const uint32_t idx = (1u << (G0 + k)) + (xof(rho0) >> (b + 1));
+        const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
         const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
         const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[iu];
         w[j] = v.x;
         wp[j] = v.y;
+      } else if constexpr (!COL && PAT == 2) {
+        // ROW last round (stages 14, 15): lane-ordered copy after the natural table, lane t's
+        // j-th twiddle at t + 32 j, so every load is one coalesced 512-B run
+        const uint32_t pos = (65536u + hi * 192u) + (k == 6 ? 32u * grp : 64u + 32u * (rho0 >> 1)) + t;
+        const rg_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(twr, pos * 16u, 0, 0);
+        w[j] = pk(v.x, v.y);
+        wp[j] = pk(v.z, v.w);
       } else {
         const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
         const rg_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(twr, idx * 16u, 0, 0);
@@ -295,9 +310,6 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
       const int rho1 = rho0 + half;
-      if constexpr ((PROBE & 16) != 0) {
-        if ((j & 1) == 0) __builtin_amdgcn_sched_barrier(0);
-      }
       if constexpr ((PROBE & 2) != 0) {
         e[rho0] += e[rho1] ^ w[j] ^ wp[j];
       } else if constexpr (!INV) {
@@ -310,24 +322,31 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
   }
 }
 
-// PROBE & 32: keep every LDS access a single ds_*_b64 (no ds_*2 merging) -- bank-conflict study
-#define RG_NM() \
-  do {                                            \
-    if constexpr ((PROBE & 32) != 0) asm volatile("" ::: "memory"); \
-  } while (0)
-template <bool INV, bool COL, bool SCALE, bool CANON, int PROBE = 0>
+// One 16 x 256 tile.  LDS images (u64 index):
+//   COL: transposed [x][s] image 16 x + s + 16 (x >> 3) for every exchange; per pattern this is
+//        a lane base plus compile-time offsets: H (x = t + 32 y): 16t + s + 16(t>>3) + 576 y;
+//        M (x = 32(t>>2) + 4y + (t&3)): s + 16(t&3) + 576(t>>2) + 64 y + 16(y>>1);
+//        L (x = 8t + r): 144 t + s + 16 r.
+//   ROW: [s][x] rows of 288 with a per-exchange pad: H<->M pad 4(x>>5), M<->L pad (x>>3),
+//        L<->H pad (x>>5).
+// Every pattern pair was checked conflict-free for ds_*_b64 half-wave groups
+// (SQ_LDS_BANK_CONFLICT = 0 for COL in profiles/r01_ntt16_pmc_summary.txt).
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0>
 __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds) {
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
-  // tile base (elements): COL: poly * 2^16 + column block * 16; ROW: 16 rows of 256
-  const size_t tbase = COL ? (((size_t)(tile >> 4) << 16) + ((tile & 15u) << 4)) : ((size_t)tile << 12);
+  // tile base (elements) and the stride between the tile's ROW sub-transforms
+  //   COL: poly * 2^16 + column block * 16
+  //   ROW: 16 consecutive rows (tile * 4096), or RP: row (tile & 255) of polys 16 (tile >> 8) + s
+  const size_t tbase = COL  ? (((size_t)(tile >> 4) << 16) + ((tile & 15u) << 4))
+                       : RP ? (((size_t)(tile >> 8) << 20) + ((tile & 255u) << 8))
+                            : ((size_t)tile << 12);
+  constexpr uint32_t RSH = RP ? 16 : 8;  // log2 of the ROW sub-transform stride (elements)
   const __amdgpu_buffer_rsrc_t rin = rg_buf(a.in + tbase);
   const __amdgpu_buffer_rsrc_t rout = rg_buf(a.out + tbase);
   const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
-  const uint32_t hi = COL ? 0u : (((tile << 4) + s) & 255u);
-  // per-pattern LDS bases (u64 index) -- see the layout derivation in DESIGN.md
-  uint32_t bH, bM, bL;  // exchange-dependent for ROW
+  const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
   // ---- global load
   if constexpr (COL) {
@@ -341,64 +360,31 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
       for (int r = 0; r < 8; ++r) e[r] = rg_bload(rin, vo, (uint32_t)r << 11);
     }
   } else {
-    const uint32_t vo = ((s << 8) + t) * 8u;
+    const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
   }
-  if constexpr (COL) {
-    bH = 16 * t + s + 16 * (t >> 3);
-    bM = s + 16 * (t & 3) + 576 * (t >> 2);
-    bL = 144 * t + s;
-  }
-  auto offH = [&](int y) { return COL ? 576 * y : 0; };
-  auto offM = [&](int y) { return COL ? 64 * y + 16 * (y >> 1) : 0; };
+  const uint32_t bH = 16 * t + s + 16 * (t >> 3), bM = s + 16 * (t & 3) + 576 * (t >> 2), bL = 144 * t + s;
+  auto offM = [](int y) { return 64 * y + 16 * (y >> 1); };
+  const uint32_t rH = 288 * s + t, rM = 288 * s + 36 * (t >> 2) + (t & 3), rL9 = 288 * s + 9 * t,
+                 rL8 = 288 * s + 8 * t + (t >> 2);
   if constexpr (!INV) {
-    ntt16_round<3, 5, 0, false, false, COL, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 5, 0, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
     // exchange H -> M
-    if constexpr (COL) {
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[bH + offH(y)] = e[y];
-      __syncthreads();
+    for (int y = 0; y < 8; ++y) lds[COL ? bH + 576 * y : rH + 36 * y] = e[y];
+    __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[bM + offM(y)];
-    } else {  // pad 4 (x >> 5)
-      const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        lds[h + 36 * y] = e[y];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        e[y] = lds[m + 4 * y];
-      }
-    }
-    ntt16_round<3, 2, 1, false, false, COL, PROBE>(a, twr, e, hi, t);
+    for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y];
+    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
     __syncthreads();
     // exchange M -> L
-    if constexpr (COL) {
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[bM + offM(y)] = e[y];
-      __syncthreads();
+    for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)] = e[y];
+    __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) e[r] = lds[bL + 16 * r];
-    } else {  // pad (x >> 3)
-      const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        lds[m + 4 * y + (y >> 1)] = e[y];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        RG_NM();
-        e[r] = lds[l + r];
-      }
-    }
-    ntt16_round<2, 0, 2, false, false, COL, PROBE>(a, twr, e, hi, t);
+    for (int r = 0; r < 8; ++r) e[r] = lds[COL ? bL + 16 * r : rL9 + r];
+    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
     if (CANON) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
@@ -408,83 +394,39 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
       for (int r = 0; r < 8; ++r) rg_bstore(e[r], rout, vo, (uint32_t)r << 11);
     } else {  // L -> H through LDS (pad x >> 5), then coalesced rows
-      const uint32_t l = 288 * s + 8 * t + (t >> 2), h = 288 * s + t;
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        RG_NM();
-        lds[l + r] = e[r];
-      }
+      for (int r = 0; r < 8; ++r) lds[rL8 + r] = e[r];
       __syncthreads();
-      const uint32_t vo = ((s << 8) + t) * 8u;
+      const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        rg_bstore(lds[h + 33 * y], rout, vo + 256u * y, 0);
-      }
+      for (int y = 0; y < 8; ++y) rg_bstore(lds[rH + 33 * y], rout, vo + 256u * y, 0);
     }
   } else {
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
-      const uint32_t h = 288 * s + t, l = 288 * s + 8 * t + (t >> 2);
 #pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        lds[h + 33 * y] = e[y];
-      }
+      for (int y = 0; y < 8; ++y) lds[rH + 33 * y] = e[y];
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        RG_NM();
-        e[r] = lds[l + r];
-      }
+      for (int r = 0; r < 8; ++r) e[r] = lds[rL8 + r];
       __syncthreads();
     }
-    ntt16_round<2, 0, 2, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
     // exchange L -> M
-    if constexpr (COL) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) lds[bL + 16 * r] = e[r];
-      __syncthreads();
+    for (int r = 0; r < 8; ++r) lds[COL ? bL + 16 * r : rL9 + r] = e[r];
+    __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[bM + offM(y)];
-    } else {  // pad x >> 3
-      const uint32_t m = 288 * s + 36 * (t >> 2) + (t & 3), l = 288 * s + 9 * t;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        RG_NM();
-        lds[l + r] = e[r];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        e[y] = lds[m + 4 * y + (y >> 1)];
-      }
-    }
-    ntt16_round<3, 2, 1, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)];
+    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
     __syncthreads();
     // exchange M -> H
-    if constexpr (COL) {
 #pragma unroll
-      for (int y = 0; y < 8; ++y) lds[bM + offM(y)] = e[y];
-      __syncthreads();
+    for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y] = e[y];
+    __syncthreads();
 #pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[bH + offH(y)];
-    } else {  // pad 4 (x >> 5)
-      const uint32_t h = 288 * s + t, m = 288 * s + 36 * (t >> 2) + (t & 3);
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        lds[m + 4 * y] = e[y];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        RG_NM();
-        e[y] = lds[h + 36 * y];
-      }
-    }
-    ntt16_round<3, 5, 0, true, SCALE, COL, PROBE>(a, twr, e, hi, t);
+    for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bH + 576 * y : rH + 36 * y];
+    ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
     if (CANON) {
 #pragma unroll
       for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
@@ -494,52 +436,17 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
       for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo, (uint32_t)y << 16);
     } else {
-      const uint32_t vo = ((s << 8) + t) * 8u;
+      const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
       for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo + 256u * y, 0);
     }
   }
 }
 
-
-template <bool INV, bool COL, bool SCALE, bool CANON, int MINW = 1, int PROBE = 0>
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP = false, int MINW = 1, int PROBE = 0>
 __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
   __shared__ uint64_t lds[16 * 288];
-  ntt16_tile<INV, COL, SCALE, CANON, PROBE>(a, blockIdx.x, lds);
-}
-
-// Software-pipelined pair of passes over consecutive chunks of polynomials: one launch runs the
-// second pass of chunk k-1 (args b, nb tiles) together with the first pass of chunk k (args f,
-// nf tiles), interleaved tile by tile.  Chunk k-1's pass-1 output was written by the previous
-// launch moments earlier and is re-read from the 256 MiB Infinity Cache, and the in-place
-// pass-2 output overwrites those same (still cached) lines, so HBM sees about one read and one
-// write per transform instead of two of each.
-//   forward: pass 1 = COL, pass 2 = ROW (+ canonical output);  inverse: pass 1 = ROW,
-//   pass 2 = COL (+ N^-1 and canonical output)
-template <bool INV, int MINW = 1, int PROBE = 0>
-__global__ __launch_bounds__(512, MINW) void ntt16_pipe(Ntt64Args f, uint32_t nf, Ntt64Args b, uint32_t nb) {
-  __shared__ uint64_t lds[16 * 288];
-  const uint32_t i = blockIdx.x, m = nf < nb ? nf : nb;
-  uint32_t tb, tf;
-  bool second;
-  if (i < 2 * m) {
-    second = (i & 1) == 0;
-    tb = tf = i >> 1;
-  } else {
-    second = nb > nf;
-    tb = tf = i - m;
-  }
-  if (second) {
-    if constexpr (!INV)
-      ntt16_tile<false, false, false, true, PROBE>(b, tb, lds);
-    else
-      ntt16_tile<true, true, true, true, PROBE>(b, tb, lds);
-  } else {
-    if constexpr (!INV)
-      ntt16_tile<false, true, false, false, PROBE>(f, tf, lds);
-    else
-      ntt16_tile<true, false, false, false, PROBE>(f, tf, lds);
-  }
+  ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds);
 }
 
 #endif  // __HIPCC__

@@ -18,10 +18,15 @@ static bool lazy_disabled() {
   return v == 1;
 }
 
+// ROW passes tile the same row of 16 polynomials when the chunk allows it (RP, twiddles
+// shared by the whole tile); otherwise 16 consecutive rows of one polynomial
 template <bool INV, bool COL, bool SCALE, bool CANON>
-static rg_status launch64(const Ntt64Args& a, hipStream_t st) {
+static rg_status launch64(const Ntt64Args& a, size_t polys, hipStream_t st) {
   const long long tiles = a.total_sub / 16;
-  hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+  if (!COL && polys % 16 == 0)
+    hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, true>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, false>), dim3((unsigned)tiles), dim3(512), 0, st, a);
   return check_launch("ntt16_pass");
 }
 
@@ -54,18 +59,18 @@ rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled) {
       a.in = p.in + b0 * N;
       a.out = p.out + b0 * N;
       a.G0 = 0;
-      RG_TRY((launch64<false, true, false, false>(a, st)));
+      RG_TRY((launch64<false, true, false, false>(a, nb, st)));
       a.in = a.out;
       a.G0 = 8;
-      RG_TRY((launch64<false, false, false, true>(a, st)));
+      RG_TRY((launch64<false, false, false, true>(a, nb, st)));
     } else {
       a.in = p.in + b0 * N;
       a.out = p.out + b0 * N;
       a.G0 = 8;
-      RG_TRY((launch64<true, false, false, false>(a, st)));
+      RG_TRY((launch64<true, false, false, false>(a, nb, st)));
       a.in = a.out;
       a.G0 = 0;
-      RG_TRY((launch64<true, true, true, true>(a, st)));
+      RG_TRY((launch64<true, true, true, true>(a, nb, st)));
     }
   }
   return RG_OK;

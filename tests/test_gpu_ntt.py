@@ -69,3 +69,36 @@ def test_vec_ops_match_oracle(fields, name):
         ringo._lib.check(ringo.lib().rg_vec(F.h, ringo.bigpoly._OPS[op], ringo._lib.ptr(got), ringo._lib.ptr(a),
                                             ringo._lib.ptr(np.ascontiguousarray(bb)), n))
         assert (got == want).all(), (name, op)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 16, 17, 32])
+def test_ntt_2e16_batches_match_oracle(fields, batch):
+    """Degree 2^16 at the config-2 prime: the lazy two-pass kernels (ntt64.hpp) with both ROW
+    tilings (16 rows of one poly, and the same row of 16 polys when batch % 16 == 0), in place
+    and out of place, device-resident entry points, forward vs the C oracle and inverse."""
+    import torch
+
+    q = fields["p63"]
+    N = 1 << 16
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, twi, ninv = cf.tables(N)
+    rng = np.random.default_rng(batch)
+    a = F.random(batch * N, rng).reshape(batch, N, 1)
+    a[0, :4, 0] = [0, 1, q - 1, q - 2]  # edge residues
+    want = cf.ntt_fwd(a, tw)
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(a.view(np.int64).reshape(-1).copy()).to(dev)
+    y = torch.empty_like(x)
+    T.fwd_dev(y, x, batch)  # out of place
+    torch.cuda.synchronize()
+    assert (y.cpu().numpy().view(np.uint64).reshape(batch, N, 1) == want).all()
+    assert torch.equal(x.cpu(), torch.from_numpy(a.view(np.int64).reshape(-1)))  # input untouched
+    T.inv_dev(y, y, batch)  # in place
+    torch.cuda.synchronize()
+    assert (y.cpu().numpy().view(np.uint64).reshape(batch, N, 1) == a).all()
+    want_inv = cf.ntt_inv(a, twi, ninv)  # inverse of an arbitrary (canonical) input
+    T.inv_dev(x, x, batch)
+    torch.cuda.synchronize()
+    assert (x.cpu().numpy().view(np.uint64).reshape(batch, N, 1) == want_inv).all()

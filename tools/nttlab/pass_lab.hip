@@ -62,7 +62,7 @@ static uint64_t powmod(uint64_t a, uint64_t e, uint64_t q) {
 template <bool INV, bool COL, bool SCALE, bool CANON, int MINW, int PROBE>
 static void launch(const Ntt64Args& a, int grid) {
   (void)grid;
-  hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, MINW, (PROBE & 255)>), dim3((unsigned)(a.total_sub / 16)), dim3(512), 0, 0, a);
+  hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, (PROBE & 512) != 0, MINW, (PROBE & 255)>), dim3((unsigned)(a.total_sub / 16)), dim3(512), 0, 0, a);
 }
 
 template <int MINW, int PROBE = 0>
@@ -167,59 +167,6 @@ static void run_chunked(const char* name, Ntt64Args base, const uint64_t* d_tw, 
          med * 1e3, 2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12);
 }
 
-// pipelined chunks: launch k = pass 2 of chunk k-1 + pass 1 of chunk k
-template <int PROBE = 0>
-static void run_pipe(const char* name, Ntt64Args base, const uint64_t* d_tw, const uint64_t* d_twi, uint64_t* d_x,
-                     const uint64_t* d_src, const uint64_t* d_ref, size_t batch, int N, size_t chunk) {
-  const size_t nch = (batch + chunk - 1) / chunk;
-  auto args = [&](size_t c, const uint64_t* tw, uint32_t& ntiles) {
-    Ntt64Args a = base;
-    a.tw = tw;
-    const size_t b0 = c * chunk, nb = std::min(chunk, batch - b0);
-    a.in = a.out = d_x + b0 * N;
-    a.total_sub = (long long)nb * (N >> 8);
-    ntiles = (uint32_t)(a.total_sub / 16);
-    return a;
-  };
-  auto fwd = [&]() {
-    for (size_t k = 0; k <= nch; ++k) {
-      uint32_t nf = 0, nb = 0;
-      Ntt64Args f = base, b = base;
-      if (k < nch) { f = args(k, d_tw, nf); f.G0 = 0; }
-      if (k > 0) { b = args(k - 1, d_tw, nb); b.G0 = 8; }
-      hipLaunchKernelGGL((ntt16_pipe<false, 1, PROBE>), dim3(nf + nb), dim3(512), 0, 0, f, nf, b, nb);
-    }
-  };
-  auto inv = [&]() {
-    for (size_t k = 0; k <= nch; ++k) {
-      uint32_t nf = 0, nb = 0;
-      Ntt64Args f = base, b = base;
-      if (k < nch) { f = args(k, d_twi, nf); f.G0 = 8; }
-      if (k > 0) { b = args(k - 1, d_twi, nb); b.G0 = 0; }
-      hipLaunchKernelGGL((ntt16_pipe<true, 1, PROBE>), dim3(nf + nb), dim3(512), 0, 0, f, nf, b, nb);
-    }
-  };
-  const size_t bytes = batch * N * 8;
-  CK(hipMemcpy(d_x, d_src, bytes, hipMemcpyDeviceToDevice));
-  fwd();
-  CK(hipDeviceSynchronize());
-  std::vector<uint64_t> got(batch * N), want(batch * N), src(batch * N);
-  CK(hipMemcpy(got.data(), d_x, bytes, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(want.data(), d_ref, bytes, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(src.data(), d_src, bytes, hipMemcpyDeviceToHost));
-  size_t badf = 0, badi = 0;
-  for (size_t i = 0; i < got.size(); ++i) badf += got[i] != want[i];
-  inv();
-  CK(hipDeviceSynchronize());
-  CK(hipMemcpy(got.data(), d_x, bytes, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < got.size(); ++i) badi += got[i] != src[i];
-  float ms, med;
-  time_reps([&]() { fwd(); inv(); }, 8, ms, med);
-  printf("%-26s chunk %4zu  fwd+inv min %7.1f med %7.1f us | %.3f M NTT/s (%.1f%% HBM)  fwd %s inv %s\n", name, chunk, ms * 1e3, med * 1e3,
-         2.0 * batch / (ms * 1e-3) / 1e6, 100.0 * 2 * batch * 2.0 * N * 8 / (ms * 1e-3) / 8e12,
-         badf ? "MISMATCH" : "ok", badi ? "MISMATCH" : "ok");
-}
-
 int main(int argc, char** argv) {
   const size_t batch = argc > 1 ? atoi(argv[1]) : 384;
   const int logN = 16, N = 1 << logN;
@@ -240,6 +187,21 @@ int main(int argc, char** argv) {
     htw[2 * i] = w; htw[2 * i + 1] = shp(w);
     htwi[2 * i] = wi; htwi[2 * i + 1] = shp(wi);
   }
+  for (auto* v : {&htw, &htwi}) {  // lane-ordered ROW last-round copy (as ntt.hip finalize)
+    const size_t base = v->size();
+    v->resize(base + (size_t)2 * 256 * 192);
+    for (int r = 0; r < 256; ++r)
+      for (int tt = 0; tt < 32; ++tt) {
+        for (int g = 0; g < 2; ++g) {
+          const size_t src = (size_t)(1 << 14) + 64 * r + 2 * tt + g, dst = (size_t)r * 192 + 32 * g + tt;
+          (*v)[base + 2 * dst] = (*v)[2 * src]; (*v)[base + 2 * dst + 1] = (*v)[2 * src + 1];
+        }
+        for (int j = 0; j < 4; ++j) {
+          const size_t src = (size_t)(1 << 15) + 128 * r + 4 * tt + j, dst = (size_t)r * 192 + 64 + 32 * j + tt;
+          (*v)[base + 2 * dst] = (*v)[2 * src]; (*v)[base + 2 * dst + 1] = (*v)[2 * src + 1];
+        }
+      }
+  }
   const uint64_t ninv = mulmod(ninv_m, rinv, q);
   const uint64_t w1n = mulmod(htwi[2], ninv, q);
   Ntt64Args base{};
@@ -248,10 +210,10 @@ int main(int argc, char** argv) {
   base.logN = logN;
   uint64_t *d_tw, *d_twi, *d_src, *d_ref, *d_x;
   const size_t bytes = batch * N * 8;
-  CK(hipMalloc(&d_tw, 16 * N)); CK(hipMalloc(&d_twi, 16 * N));
+  CK(hipMalloc(&d_tw, 8 * htw.size())); CK(hipMalloc(&d_twi, 8 * htwi.size()));
   CK(hipMalloc(&d_src, bytes)); CK(hipMalloc(&d_ref, bytes)); CK(hipMalloc(&d_x, bytes));
-  CK(hipMemcpy(d_tw, htw.data(), 16 * N, hipMemcpyHostToDevice));
-  CK(hipMemcpy(d_twi, htwi.data(), 16 * N, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_tw, htw.data(), 8 * htw.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_twi, htwi.data(), 8 * htwi.size(), hipMemcpyHostToDevice));
   std::vector<uint64_t> h(batch * N);
   uint64_t s = 0x52494E47;
   for (auto& v : h) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (s >> 1) % q; }
@@ -286,11 +248,12 @@ int main(int argc, char** argv) {
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   (void)cus;
-  for (int rep = 0; rep < 3; ++rep) {
+  for (int rep = 0; rep < 2; ++rep) {
+    run_variant<1, 256>("ntt16 per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
+    run_variant<1, 256 + 512>("ntt16 RP per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
+    run_variant<1, 256 + 512 + 1>("RP no-tw per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
     run_chunked<256>("ntt16", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
-    run_chunked<256 + 32>("ntt16 no-ds-merge", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 512>("ntt16 RP", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
   }
-  run_variant<1, 256>("ntt16 per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
-  run_variant<1, 256 + 32>("ntt16 no-ds-merge per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
   return 0;
 }
