@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--logn", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the L=4 / Jindo lines")
+    ap.add_argument("--extra", default="l4,j14,j16", help="secondary lines to run: l4, j14, j16 (comma list)")
+    ap.add_argument("--j14-batch", type=int, default=256, help="commits per GPU per step, configs[2] shape")
+    ap.add_argument("--j16-batch", type=int, default=512,
+                    help="commits per GPU per step, configs[4] shape (4096 commits / 8 GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
@@ -213,6 +217,32 @@ def traffic_per_ntt():
         return None
 
 
+def vec_mul_bench(torch, ringo, q, L, n, steps, seed):
+    """configs[3]'s pointwise product: MulTo of two NTT-domain polys (base_op.go:133-142) over n
+    elements, device-resident; bytes = 2 reads + 1 write of 8L B per element."""
+    from ringo.bigpoly import vec_dev
+    dev = torch.device("cuda", torch.cuda.current_device())
+    F = ringo.Field(q)
+    a = torch.from_numpy(uniform_elems(q, L, n, seed).view(np.int64).reshape(-1)).to(dev)
+    b = torch.from_numpy(uniform_elems(q, L, n, seed + 1).view(np.int64).reshape(-1)).to(dev)
+    out = torch.empty_like(a)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        vec_dev(F, "mul", out, a, b, n, stream)
+
+    prewarm(torch, step, 0.1)
+    torch.cuda.synchronize()
+    ev = Events(torch, stream)
+    ev.start()
+    for _ in range(steps):
+        step()
+    ev.stop()
+    torch.cuda.synchronize()
+    ms = ev.total_ms() / steps
+    return dict(elems_per_s=n / (ms * 1e-3), achieved_GBs=3 * 8 * L * n / (ms * 1e-3) / 1e9, ms=ms)
+
+
 def cpu_baseline(q, L, logn, seconds):
     """C restatement (oracle/liboracle.so) fwd+inv on this host: bounded sample, all threads
     the OpenMP runtime gives it (OMP_NUM_THREADS)."""
@@ -293,15 +323,24 @@ def main():
                                      "pass-1 -> pass-2 intermediate makes a round trip, 2x algorithmic"},
         "selfcheck_fwd_inv_identity": ok,
     }
-    if not args.no_extra:
+    extra = set() if args.no_extra else set(x for x in args.extra.split(",") if x)
+    if "l4" in extra:
         r4 = ntt_step_bench(torch, ringo, dist, Q255, 4, 64, args.logn, max(2, args.steps // 2), 1, 7 + rank)
         ms4 = r4["wall_s"] * 1000.0 / max(2, args.steps // 2)
+        if dist is not None:
+            t = torch.tensor([ms4], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms4 = float(t[0])
+        vm = vec_mul_bench(torch, ringo, Q255, 4, 64 * N, 10, 11 + rank)
         out["l4_ntt"] = {"value": world * 2 * 64 / (ms4 / 1000.0), "unit": "NTT/s",
                          "config": "configs[3]: fwd+inv negacyclic NTT, N=2^16, 255-bit Jindo prime, batch 64/GPU",
+                         "kernel": "ntt256_pass (4-limb Montgomery, q = 1 mod 2^64; VALU-bound)",
                          "achieved_GBs": 2 * N * 32 * r4["ntts"] / (r4["kernel_ms"] / 1000.0) / 1e9,
-                         "selfcheck_fwd_inv_identity": r4["ok"]}
-    if not args.no_extra:
-        for cfg, jb in (("t14_b1", 64), ("t16_b4096", 16)):
+                         "selfcheck_fwd_inv_identity": r4["ok"],
+                         "pointwise_mul": {"unit": "elements/s", "value": world * vm["elems_per_s"],
+                                           "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N}}
+    for cfg, jb, key in (("t14_b1", args.j14_batch, "j14"), ("t16_b4096", args.j16_batch, "j16")):
+        if key in extra:
             jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world)
             jms = jr["wall_s"] * 1000.0 / max(2, args.steps // 2)
             if dist is not None:

@@ -30,6 +30,7 @@
 #include "common.hpp"
 #include "field.hpp"
 #include "host_field.hpp"
+#include "ntt64.hpp"
 
 namespace rg {
 
@@ -239,6 +240,7 @@ struct PrepArgs {
   uint64_t* enc;               // [B][cols+1][rows][nq][d]
   uint64_t* mlwe;              // [B][cols+1][nm][nq][d]
   long long n_enc;             // B * (cols+1) * rows
+  long long n_ml;              // B * (cols+1) * (inMSIS + mlwe)
 };
 
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -300,6 +302,146 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     ntt_lds(poly[lc], d, a.R.fwd + (long long)lc * d, a.R.p[lc].q, tid % half, half, active);
   }
   for (int k = tid; k < nq * d; k += blockDim.x) dst[k] = poly[k / d][k % d];
+}
+
+// Wave-per-polynomial prep for d = 256 (every Jindo parameter set): one wave owns one job and two
+// RNS limbs at a time (lanes 0-31 limb l0, 32-63 limb l0+1), 8 coefficients per lane; the
+// 256-point negacyclic NTT runs as rounds of 3 + 3 + 2 radix-2 stages in registers with
+// wave-local LDS exchanges (no workgroup barrier; ntt64.hpp's ROW index algebra with hi = 0),
+// lazy [0, 2q) Shoup arithmetic, canonical output.  Same results as prep_kernel.
+constexpr int kPrepWaves = 4;
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+template <int RK, int LO, int PAT>
+__device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, const Q64& Q, uint32_t t) {
+  auto xof = [&](int rho) -> uint32_t {
+    if (PAT == 0) return t + 32u * rho;
+    if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
+    return 8u * t + rho;
+  };
+  constexpr int NPK = 1 << RK;
+#pragma unroll
+  for (int sp = 0; sp < RK; ++sp) {
+    const int bw = RK - 1 - sp, b = LO + bw, k = 7 - b, half = 1 << bw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int grp = j / (NPK / 2), jj = j % (NPK / 2);
+      const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
+      const ulonglong2 w = roots[(1u << k) + (xof(rho0) >> (b + 1))];
+      const uint64_t tt = shoup_mul_lazy(e[rho0 + half], w.x, w.y, Q.q);
+      const uint64_t x = e[rho0];
+      e[rho0] = lazy_add(x, tt, Q);
+      e[rho0 + half] = lazy_sub(x, tt, Q);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
+  __shared__ uint64_t lds_all[kPrepWaves][2 * 288];
+  const JShape& S = a.s;
+  const int nq = S.nq;
+  const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* lds = lds_all[wv];
+  const long long job = (long long)blockIdx.x * kPrepWaves + wv;
+  if (job >= a.n_enc + a.n_ml) return;
+  const bool is_enc = job < a.n_enc;
+  uint64_t* dst;
+  const uint32_t* dg = nullptr;
+  const long long* nz;
+  if (is_enc) {
+    const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
+    dst = a.enc + job * nq * 256;
+    if (a.skip[cr]) {  // reference leaves Opening.Encode[i][j] at zero (prover.go:103-105,121-123)
+      for (int k = (int)lane; k < nq * 256; k += 64) dst[k] = 0;
+      return;
+    }
+    dg = a.digits + job * 256;
+    nz = a.enc_noise + job * 256;
+  } else {
+    const long long mj = job - a.n_enc;
+    dst = a.mlwe + mj * nq * 256;
+    nz = a.mlwe_noise + mj * 256;
+  }
+  // per-lane inputs for x = t + 32 y (shared by both limbs of the pair)
+  long long c[8], cs[8];
+  uint32_t dgk[8];
+#pragma unroll
+  for (int y = 0; y < 8; ++y) {
+    const int k = (int)t + 32 * y;
+    c[y] = nz[k];
+    if (is_enc) {
+      const int ks = k - S.slots;
+      cs[y] = ks >= 0 ? nz[ks] : nz[ks + 256];
+      dgk[y] = dg[k];
+    }
+  }
+  for (int l0 = 0; l0 < nq; l0 += 2) {
+    const int limb = l0 + (int)hs;
+    const bool active = limb < nq;
+    const int lc = active ? limb : l0;
+    const RnsPrime& P = a.R.p[lc];
+    Q64 Q = make_q64(P.q);
+    const ulonglong2* roots = a.R.fwd + (long long)lc * 256;
+    uint64_t e[8];
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+      const uint64_t q = P.q;
+      // MForm is multiplication by 2^64 mod q, so the encode tail MForm(dg) + MForm(+-s') -
+      // MForm(s) b (encoder.go:184-199) is MForm of one small signed integer; Shoup accepts any
+      // 64-bit input, so MForm(|v|) needs no prior reduction.  Same residues as the per-term form.
+      long long v = c[y];
+      bool small = true;
+      if (is_enc) {
+        const int k = (int)t + 32 * y;
+        const long long s2 = k < S.slots ? -cs[y] : cs[y];  // wrapped coefficients negate (:191-195)
+        const long long lim = 1LL << 40;
+        small = v > -lim && v < lim && s2 > -lim && s2 < lim;
+        v = (long long)dgk[y] + s2 - v * (long long)S.base;
+      }
+      if (small) {
+        const uint64_t av = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+        const uint64_t m = sh_mul(av, P.r64, P.r64_sh, q);
+        e[y] = v < 0 ? mod_neg(m, q) : m;
+      } else {  // huge injected noise: the reference's per-term form
+        const int k = (int)t + 32 * y;
+        const uint64_t sm = sh_mul(signed_residue(c[y], q), P.r64, P.r64_sh, q);
+        uint64_t sh = sh_mul(signed_residue(cs[y], q), P.r64, P.r64_sh, q);
+        if (k < S.slots) sh = mod_neg(sh, q);
+        sh = mod_sub(sh, sh_mul(sm, P.bmod, P.bmod_sh, q), q);
+        e[y] = mod_add(sh_mul(dgk[y], P.r64, P.r64_sh, q), sh, q);
+      }
+    }
+    // NTT: H round (stages 0-2), H->M, M round (3-5), M->L, L round (6-7), L->H, store
+    const uint32_t rH = 288 * hs + t, rM = 288 * hs + 36 * (t >> 2) + (t & 3), rL9 = 288 * hs + 9 * t,
+                   rL8 = 288 * hs + 8 * t + (t >> 2);
+    prep_round<3, 5, 0>(e, roots, Q, t);
+#pragma unroll
+    for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = lds[rM + 4 * y];
+    prep_round<3, 2, 1>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) lds[rM + 4 * y + (y >> 1)] = e[y];
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) e[r] = lds[rL9 + r];
+    prep_round<2, 0, 2>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) lds[rL8 + r] = canon(e[r], Q);
+    wave_lds_fence();
+    if (active) {
+      uint64_t* o = dst + (long long)limb * 256;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) o[t + 32 * y] = lds[rH + 33 * y];
+    }
+    wave_lds_fence();
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -829,6 +971,16 @@ static rg_status ensure_scratch(rg_jindo* J, size_t batch) {
   return RG_OK;
 }
 
+// RINGO_JINDO_PREP=legacy selects the workgroup-per-polynomial prep kernel (A/B switch)
+static bool prep_legacy() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RINGO_JINDO_PREP");
+    v = (e && e[0] == 'l') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
                             const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
                             uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
@@ -875,7 +1027,12 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   pa.mlwe = d_mlwe;
   pa.n_enc = (long long)batch * (p.cols + 1) * p.rows;
   const long long n_ml = (long long)batch * (p.cols + 1) * nm;
-  hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
+  pa.n_ml = n_ml;
+  if (d == 256 && !prep_legacy())
+    hipLaunchKernelGGL(prep256_kernel, dim3((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)),
+                       dim3(64 * kPrepWaves), 0, st, pa);
+  else
+    hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   RG_TRY(check_launch("jindo prep"));
   // 3. inner MAC
   MacArgs ma;

@@ -228,7 +228,11 @@ static rg_status run(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t 
       return done ? RG_OK : ntt_run_L1(p, st);
     }
     case 2: return ntt_run_L2(p, st);
-    case 4: return ntt_run_L4(p, st);
+    case 4: {
+      bool done = false;
+      RG_TRY(ntt256_run(p, st, &done));
+      return done ? RG_OK : ntt_run_L4(p, st);
+    }
     case 7: return ntt_run_L7(p, st);
     case 14: return ntt_run_L14(p, st);
     default: return RG_ERR_UNSUPPORTED;

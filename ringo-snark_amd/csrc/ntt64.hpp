@@ -25,7 +25,7 @@ struct Q64 {
   uint32_t qlo1;   // q mod 2^32 == 1
 };
 
-inline Q64 make_q64(uint64_t q) {
+RG_HD Q64 make_q64(uint64_t q) {
   Q64 Q;
   Q.q = q;
   Q.q2 = 2 * q;

@@ -29,6 +29,8 @@ struct NttLaunch {
 rg_status ntt_run_L1(const NttLaunch& p, hipStream_t st);
 // lazy single-word pass kernels (ntt_l1_lazy.hip); sets *handled when the shape is covered
 rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled);
+// 4-limb degree-2^16 kernels for q = 1 mod 2^64 (ntt_l4_fast.hip)
+rg_status ntt256_run(const NttLaunch& p, hipStream_t st, bool* handled);
 rg_status ntt_run_L2(const NttLaunch& p, hipStream_t st);
 rg_status ntt_run_L4(const NttLaunch& p, hipStream_t st);
 rg_status ntt_run_L7(const NttLaunch& p, hipStream_t st);

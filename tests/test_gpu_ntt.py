@@ -102,3 +102,23 @@ def test_ntt_2e16_batches_match_oracle(fields, batch):
     T.inv_dev(x, x, batch)
     torch.cuda.synchronize()
     assert (x.cpu().numpy().view(np.uint64).reshape(batch, N, 1) == want_inv).all()
+
+
+@pytest.mark.parametrize("batch", [1, 4, 5])
+def test_ntt_2e16_q255_matches_oracle(fields, batch):
+    """Degree 2^16 at the Jindo default prime (4 limbs, q = 1 mod 2^64): the ntt256 kernels
+    (both ROW tilings: same row of 4 polys when batch % 4 == 0, else 4 rows of one poly),
+    forward vs the C oracle, inverse round trip and inverse of arbitrary input."""
+    q = fields["jindo_zp"]
+    N = 1 << 16
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, twi, ninv = cf.tables(N)
+    rng = np.random.default_rng(100 + batch)
+    a = F.random(batch * N, rng).reshape(batch, N, F.L)
+    a[0, 0] = F.mont([q - 1])[0]
+    got = T.FwdNTTTo(None, a)
+    assert (got == cf.ntt_fwd(a, tw)).all()
+    assert (T.InvNTTTo(None, got) == a).all()
+    assert (T.InvNTTTo(None, a) == cf.ntt_inv(a, twi, ninv)).all()
