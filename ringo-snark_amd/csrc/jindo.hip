@@ -241,6 +241,7 @@ struct PrepArgs {
   uint64_t* mlwe;              // [B][cols+1][nm][nq][d]
   long long n_enc;             // B * (cols+1) * rows
   long long n_ml;              // B * (cols+1) * (inMSIS + mlwe)
+  long long clim;              // |noise| bound for the one-integer encode form: 2^61 / base
 };
 
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -315,7 +316,8 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("" ::: "memory");
 }
 template <int RK, int LO, int PAT>
-__device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, const Q64& Q, uint32_t t) {
+__device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, uint64_t q, uint64_t q2,
+                                           uint32_t t) {
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
@@ -330,12 +332,21 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
       const ulonglong2 w = roots[(1u << k) + (xof(rho0) >> (b + 1))];
-      const uint64_t tt = shoup_mul_lazy(e[rho0 + half], w.x, w.y, Q.q);
-      const uint64_t x = e[rho0];
-      e[rho0] = lazy_add(x, tt, Q);
-      e[rho0 + half] = lazy_sub(x, tt, Q);
+      // Harvey: values in [0, 4q) (ring primes are < 2^62), twiddle product in [0, 2q)
+      uint64_t x = e[rho0];
+      x = x >= q2 ? x - q2 : x;
+      const uint64_t tt = shoup_mul_lazy(e[rho0 + half], w.x, w.y, q);
+      e[rho0] = x + tt;
+      e[rho0 + half] = x + q2 - tt;
     }
   }
+}
+
+// signed integer -> residue in [0, q) without division (Shoup by 1 reduces any 64-bit value)
+__device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
+  const uint64_t ac = c < 0 ? (uint64_t)(-(c + 1)) + 1 : (uint64_t)c;
+  const uint64_t m = sh_mul(ac, 1, P.one_sh, P.q);
+  return c < 0 ? mod_neg(m, P.q) : m;
 }
 
 __global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
@@ -365,75 +376,77 @@ __global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
     dst = a.mlwe + mj * nq * 256;
     nz = a.mlwe_noise + mj * 256;
   }
-  // per-lane inputs for x = t + 32 y (shared by both limbs of the pair)
-  long long c[8], cs[8];
-  uint32_t dgk[8];
+  // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
+  // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
+  // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  v is limb independent.
+  long long v[8];
+  uint32_t big = 0;  // bit y: coefficient t + 32 y needs the term-by-term form
 #pragma unroll
   for (int y = 0; y < 8; ++y) {
     const int k = (int)t + 32 * y;
-    c[y] = nz[k];
+    const long long c = nz[k];
     if (is_enc) {
       const int ks = k - S.slots;
-      cs[y] = ks >= 0 ? nz[ks] : nz[ks + 256];
-      dgk[y] = dg[k];
+      const long long cs = ks >= 0 ? nz[ks] : nz[ks + 256];
+      const uint64_t s2 = k < S.slots ? 0ull - (uint64_t)cs : (uint64_t)cs;  // wrapped coefficients negate
+      const bool ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
+      big |= ok ? 0u : (1u << y);
+      v[y] = (long long)((uint64_t)dg[k] + s2 - (uint64_t)c * S.base);
+    } else {
+      v[y] = c;
     }
   }
+  const uint32_t rH = 288 * hs + t, rM = 288 * hs + 36 * (t >> 2) + (t & 3), rL9 = 288 * hs + 9 * t,
+                 rL8 = 288 * hs + 8 * t + (t >> 2);
   for (int l0 = 0; l0 < nq; l0 += 2) {
     const int limb = l0 + (int)hs;
     const bool active = limb < nq;
     const int lc = active ? limb : l0;
     const RnsPrime& P = a.R.p[lc];
-    Q64 Q = make_q64(P.q);
+    const uint64_t q = P.q, q2 = 2 * q;
     const ulonglong2* roots = a.R.fwd + (long long)lc * 256;
     uint64_t e[8];
 #pragma unroll
     for (int y = 0; y < 8; ++y) {
-      const uint64_t q = P.q;
-      // MForm is multiplication by 2^64 mod q, so the encode tail MForm(dg) + MForm(+-s') -
-      // MForm(s) b (encoder.go:184-199) is MForm of one small signed integer; Shoup accepts any
-      // 64-bit input, so MForm(|v|) needs no prior reduction.  Same residues as the per-term form.
-      long long v = c[y];
-      bool small = true;
-      if (is_enc) {
-        const int k = (int)t + 32 * y;
-        const long long s2 = k < S.slots ? -cs[y] : cs[y];  // wrapped coefficients negate (:191-195)
-        const long long lim = 1LL << 40;
-        small = v > -lim && v < lim && s2 > -lim && s2 < lim;
-        v = (long long)dgk[y] + s2 - v * (long long)S.base;
-      }
-      if (small) {
-        const uint64_t av = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-        const uint64_t m = sh_mul(av, P.r64, P.r64_sh, q);
-        e[y] = v < 0 ? mod_neg(m, q) : m;
-      } else {  // huge injected noise: the reference's per-term form
-        const int k = (int)t + 32 * y;
-        const uint64_t sm = sh_mul(signed_residue(c[y], q), P.r64, P.r64_sh, q);
-        uint64_t sh = sh_mul(signed_residue(cs[y], q), P.r64, P.r64_sh, q);
-        if (k < S.slots) sh = mod_neg(sh, q);
-        sh = mod_sub(sh, sh_mul(sm, P.bmod, P.bmod_sh, q), q);
-        e[y] = mod_add(sh_mul(dgk[y], P.r64, P.r64_sh, q), sh, q);
+      const long long vy = v[y];
+      const uint64_t av = vy < 0 ? (uint64_t)(-(vy + 1)) + 1 : (uint64_t)vy;
+      const uint64_t m = sh_mul(av, P.r64, P.r64_sh, q);  // Shoup: exact for any 64-bit input
+      e[y] = vy < 0 ? mod_neg(m, q) : m;
+    }
+    if (big) {  // rare (huge injected noise): every term reduced separately, same residue
+      for (int y = 0; y < 8; ++y) {
+        if (!((big >> y) & 1u)) continue;
+        const int k = (int)t + 32 * y, ks = k - S.slots;
+        const uint64_t cm = red_signed(nz[k], P);
+        uint64_t s2 = red_signed(ks >= 0 ? nz[ks] : nz[ks + 256], P);
+        if (k < S.slots) s2 = mod_neg(s2, q);
+        uint64_t val = mod_add(sh_mul(dg[k], 1, P.one_sh, q), s2, q);
+        val = mod_sub(val, sh_mul(cm, P.bmod, P.bmod_sh, q), q);
+        e[y] = sh_mul(val, P.r64, P.r64_sh, q);
       }
     }
     // NTT: H round (stages 0-2), H->M, M round (3-5), M->L, L round (6-7), L->H, store
-    const uint32_t rH = 288 * hs + t, rM = 288 * hs + 36 * (t >> 2) + (t & 3), rL9 = 288 * hs + 9 * t,
-                   rL8 = 288 * hs + 8 * t + (t >> 2);
-    prep_round<3, 5, 0>(e, roots, Q, t);
+    prep_round<3, 5, 0>(e, roots, q, q2, t);
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[rM + 4 * y];
-    prep_round<3, 2, 1>(e, roots, Q, t);
+    prep_round<3, 2, 1>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rM + 4 * y + (y >> 1)] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[rL9 + r];
-    prep_round<2, 0, 2>(e, roots, Q, t);
+    prep_round<2, 0, 2>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) lds[rL8 + r] = canon(e[r], Q);
+    for (int r = 0; r < 8; ++r) {  // [0, 4q) -> [0, q)
+      uint64_t x = e[r];
+      x = x >= q2 ? x - q2 : x;
+      lds[rL8 + r] = x >= q ? x - q : x;
+    }
     wave_lds_fence();
     if (active) {
       uint64_t* o = dst + (long long)limb * 256;
@@ -587,6 +600,192 @@ static rg_status launch_mac(const MacArgs& m, hipStream_t st) {
   return RG_OK;
 }
 
+// Split-accumulator MAC for primes q < 2^60 (every Jindo ring prime of the configs): with
+// 29-bit low halves a = a0 + a1 2^29 (the commit key is stored pre-split, a0 | a1 << 32) and
+// b = b0 + b1 2^29, a*b = a0b0 + (a0b1 + a1b0) 2^29 + a1b1 2^58, so three 64-bit accumulators
+// absorb `fold` terms (host-computed so no partial sum can wrap) with plain v_mad_u64_u32 (no
+// carries: 4 VALU per MAC instead of ~11) before folding into the exact 128-bit sum.  The sum
+// is the same integer as Acc's, so the reduction and the result are identical.
+// Lanes: lane = jb + nJB * lkl (nJB in {1,2,4,8} output blocks of JB rows share each data word
+// load; 64 / nJB consecutive (limb, coeff) per wave).  The kMac2Waves waves of a workgroup
+// take the SAME (limb, coeff) block and consecutive column groups, so their commit-key loads
+// are the same lines, served by the CU's L1 instead of once per wave from L2.
+constexpr int kMac2Waves = 4;
+struct Mac2Acc {
+  uint64_t s00, s01, s11, lo, hi;
+};
+__device__ __forceinline__ void mac2_fold(Mac2Acc& a) {
+  uint32_t c0 = 0, c1 = 0, c2 = 0;
+  a.lo = addc(a.lo, a.s00, c0);
+  a.lo = addc(a.lo, a.s01 << 29, c1);
+  a.lo = addc(a.lo, a.s11 << 58, c2);
+  a.hi += (a.s01 >> 35) + (a.s11 >> 6) + c0 + c1 + c2;
+  a.s00 = a.s01 = a.s11 = 0;
+}
+
+template <int JB, int NC>
+__global__ __launch_bounds__(64 * kMac2Waves) void mac2_kernel(MacArgs a, int nJB, int fold) {
+  const long long per_col = (long long)a.nl * a.d;
+  const long long ngroups = (a.ncols + NC - 1) / NC;
+  const int lkw = 64 / nJB;
+  const int lane = (int)(threadIdx.x & 63);
+  const long long wpc = per_col / lkw;  // (limb, coeff) blocks per column group
+  const long long cg = (blockIdx.x / wpc) * kMac2Waves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (cg >= ngroups) return;
+  const long long lkb = blockIdx.x % wpc;
+  const int jb = lane % nJB;
+  const int lk = (int)lkb * lkw + lane / nJB;
+  const int l = lk / a.d;
+  const int j0 = jb * JB;
+  const int J = min(JB, a.J - j0);  // may be <= 0 for padding lanes
+  const long long col0 = cg * NC;
+  const int nc = (int)min((long long)NC, a.ncols - col0);
+  Mac2Acc acc[NC][JB];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) acc[c][j] = Mac2Acc{0, 0, 0, 0, 0};
+  for (int set = 0; set < 2; ++set) {
+    const int T = set ? a.T2 : a.T1;
+    if (!T) continue;
+    // buffer addressing: per-lane offsets, per-term strides in SGPRs; the next term's words
+    // are loaded while the current term is multiplied (one term of prefetch)
+    const __amdgpu_buffer_rsrc_t ra = rg_buf(set ? a.A2 : a.A1);
+    const uint32_t astride = (uint32_t)(per_col * 8);
+    const long long bcol = set ? a.b2_col : a.b1_col, bterm = set ? a.b2_term : a.b1_term;
+    const uint64_t* Bb = set ? a.B2 : a.B1;
+    __amdgpu_buffer_rsrc_t rb[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {  // wave-uniform base, so the resource lives in SGPRs
+      const uint64_t pb = (uint64_t)(Bb + (col0 + (c < nc ? c : 0)) * bcol);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
+      rb[c] = rg_buf((const void*)(((uint64_t)hi << 32) | lo));
+    }
+    const uint32_t bvo = (uint32_t)lk * 8u, bstride = (uint32_t)(bterm * 8);
+    // padding rows (j >= J) and columns (c >= nc) load valid words and are never stored, so
+    // every load is unconditional
+    uint32_t avj[JB];
+#pragma unroll
+    for (int j = 0; j < JB; ++j) avj[j] = (uint32_t)(((long long)min(j0 + j, a.J - 1) * T * per_col + lk) * 8);
+    auto load = [&](int t, uint64_t (&x)[JB], uint64_t (&y)[NC]) {
+#pragma unroll
+      for (int j = 0; j < JB; ++j) x[j] = rg_bload(ra, avj[j], (uint32_t)t * astride);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[c] = rg_bload(rb[c], bvo, (uint32_t)t * bstride);
+    };
+    auto madd = [&](const uint64_t (&x)[JB], const uint64_t (&y)[NC]) {
+      uint32_t b0[NC], b1[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        b0[c] = (uint32_t)y[c] & 0x1fffffffu;
+        b1[c] = (uint32_t)(y[c] >> 29);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          const uint32_t a0 = (uint32_t)x[j], a1 = (uint32_t)(x[j] >> 32);
+          Mac2Acc& z = acc[c][j];
+          z.s00 = mad64(a0, b0[c], z.s00);
+          z.s01 = mad64(a0, b1[c], z.s01);
+          z.s01 = mad64(a1, b0[c], z.s01);
+          z.s11 = mad64(a1, b1[c], z.s11);
+        }
+    };
+    for (int t0 = 0; t0 < T; t0 += fold) {
+      const int t1 = min(T, t0 + fold);
+      int t = t0;
+      // two terms per trip, ping-pong buffers: the loads of term t+1 are in flight while term t
+      // is multiplied, with no register copies
+      uint64_t xa[JB], ya[NC], xb[JB], yb[NC];
+      load(t, xa, ya);
+      for (; t + 1 < t1; t += 2) {
+        load(t + 1, xb, yb);
+        madd(xa, ya);
+        if (t + 2 < t1) load(t + 2, xa, ya);
+        madd(xb, yb);
+      }
+      if (t < t1) madd(xa, ya);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < JB; ++j) mac2_fold(acc[c][j]);
+    }
+  }
+  const RnsPrime& P = a.P[l];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c >= nc) continue;
+    const long long col = col0 + c;
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      if (j >= J) continue;
+      const uint64_t q = P.q;
+      uint64_t r = sh_mul(acc[c][j].lo, P.rinv, P.rinv_sh, q);
+      r = mod_add(r, sh_mul(acc[c][j].hi, 1, P.one_sh, q), q);
+      if (a.C) r = mod_add(a.C[col * a.c_col + (long long)(j0 + j) * a.c_j + lk], r, P.q);
+      a.out[(col * a.J + j0 + j) * per_col + lk] = r;
+    }
+  }
+}
+
+constexpr int kMac2NC = 2;
+template <int JB>
+static rg_status launch_mac2_jb(const MacArgs& m, int nJB, int fold, hipStream_t st) {
+  const long long groups = (m.ncols + kMac2NC - 1) / kMac2NC;
+  const long long wpc = (long long)(m.nl * m.d) / (64 / nJB);
+  const long long blocks = (groups + kMac2Waves - 1) / kMac2Waves * wpc;
+  hipLaunchKernelGGL((mac2_kernel<JB, kMac2NC>), dim3((unsigned)blocks), dim3(64 * kMac2Waves), 0, st, m, nJB, fold);
+  return check_launch("jindo mac2");
+}
+
+// fold period: the largest F <= 32 with F * max partial product < 2^64 in every accumulator
+// (a0 b0 < 2^58, two of a0 b1, a1 b0 < 2^bits per term, a1 b1 < 2^(2 (bits - 29)))
+static int mac2_fold(const MacArgs& m) {
+  int bits = 29;
+  for (int l = 0; l < m.nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(m.P[l].q - 1));
+  int f = 32;
+  while (f > 1 && ((double)f * 2.0 * std::ldexp(1.0, bits) > std::ldexp(1.0, 64) ||
+                   (double)f * std::ldexp(1.0, 2 * std::max(0, bits - 29)) > std::ldexp(1.0, 64)))
+    f >>= 1;
+  return f;
+}
+
+// eligible: primes < 2^60 with a fold period >= 4, the sum fits 128 bits, and 64 (limb, coeff)
+// lanes tile a column
+static bool mac2_ok(const MacArgs& m) {
+  for (int l = 0; l < m.nl; ++l)
+    if (m.P[l].q >> 60) return false;
+  int bits = 0;
+  for (int l = 0; l < m.nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(m.P[l].q - 1));
+  const bool fits128 = (double)(m.T1 + m.T2) * std::ldexp(1.0, 2 * bits) < std::ldexp(1.0, 128);
+  // measured: ahead of mac_kernel at J <= 10 (one shared data load per 2 lanes); at J = 16 the
+  // 4-lane sharing makes it load-issue bound and slower than mac_kernel
+  return mac2_fold(m) >= 4 && fits128 && (m.nl * m.d) % 64 == 0 && m.J <= 10;
+}
+
+static rg_status launch_mac2(const MacArgs& m, hipStream_t st) {
+  const int fold = mac2_fold(m);
+  static const int maxjb = [] {  // RINGO_JINDO_MAC2_JB: outputs per lane (tuning)
+    const char* e = getenv("RINGO_JINDO_MAC2_JB");
+    return e ? std::max(1, std::min(5, atoi(e))) : 5;
+  }();
+  int nJB = 1;
+  while (nJB < 8 && (m.J + nJB - 1) / nJB > maxjb) nJB *= 2;
+  switch ((m.J + nJB - 1) / nJB) {
+    case 1: return launch_mac2_jb<1>(m, nJB, fold, st);
+    case 2: return launch_mac2_jb<2>(m, nJB, fold, st);
+    case 3: return launch_mac2_jb<3>(m, nJB, fold, st);
+    case 4: return launch_mac2_jb<4>(m, nJB, fold, st);
+    default: return launch_mac2_jb<5>(m, nJB, fold, st);
+  }
+}
+
+// host: the commit key in split form (a & (2^29 - 1)) | (a >> 29) << 32
+static void split29(std::vector<uint64_t>& v) {
+  for (auto& x : v) x = (x & 0x1fffffffull) | ((x >> 29) << 32);
+}
+
 // ------------------------------------------------------------------------------------------
 // 4. round: IMForm -> INTT -> centred CRT -> floor shift -> mod q' -> MForm -> NTT
 // ------------------------------------------------------------------------------------------
@@ -722,6 +921,8 @@ struct rg_jindo {
   rg::DstDev dst_o;
   std::vector<uint64_t> h_ck_in, h_ck_mlwe, h_ck_out;
   rg::DevBuf ck_in, ck_mlwe, ck_out;
+  rg::DevBuf ck_in_s, ck_mlwe_s, ck_out_s;  // 29-bit split copies for mac2_kernel (primes < 2^60)
+  bool split_q = false, split_o = false;
   uint64_t base_inv;
   std::mutex mu;  // guards the scratch cache
   rg::DevBuf s_digits, s_com, s_ocom, s_skip;
@@ -1028,6 +1229,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   pa.n_enc = (long long)batch * (p.cols + 1) * p.rows;
   const long long n_ml = (long long)batch * (p.cols + 1) * nm;
   pa.n_ml = n_ml;
+  pa.clim = (long long)(((uint64_t)1 << 61) / p.base);
   if (d == 256 && !prep_legacy())
     hipLaunchKernelGGL(prep256_kernel, dim3((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)),
                        dim3(64 * kPrepWaves), 0, st, pa);
@@ -1056,7 +1258,13 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   ma.c_j = (long long)nq * d;
   ma.out = J->s_com.as<uint64_t>();
   for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
-  RG_TRY(launch_mac(ma, st));
+  if (J->split_q && mac2_ok(ma)) {
+    ma.A1 = J->ck_in_s.as<uint64_t>();
+    ma.A2 = J->ck_mlwe_s.as<uint64_t>();
+    RG_TRY(launch_mac2(ma, st));
+  } else {
+    RG_TRY(launch_mac(ma, st));
+  }
   // 4. inner round -> Opening.InCommit (column i, j -> index i*inMSIS + j)
   RoundArgs ra;
   memset(&ra, 0, sizeof(ra));
@@ -1089,7 +1297,12 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   mo.b1_term = (long long)nqo * d;
   mo.out = J->s_ocom.as<uint64_t>();
   for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
-  RG_TRY(launch_mac(mo, st));
+  if (J->split_o && mac2_ok(mo)) {
+    mo.A1 = J->ck_out_s.as<uint64_t>();
+    RG_TRY(launch_mac2(mo, st));
+  } else {
+    RG_TRY(launch_mac(mo, st));
+  }
   RoundArgs ro = ra;
   ro.cut = p.log_out_cut;
   ro.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
@@ -1127,6 +1340,24 @@ static rg_status upload_ck(rg_jindo* J) {
   RG_TRY(J->ck_in.upload(J->h_ck_in.data(), J->h_ck_in.size() * 8));
   if (!J->h_ck_mlwe.empty()) RG_TRY(J->ck_mlwe.upload(J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8));
   RG_TRY(J->ck_out.upload(J->h_ck_out.data(), J->h_ck_out.size() * 8));
+  J->split_q = J->split_o = getenv("RINGO_JINDO_MAC") == nullptr || getenv("RINGO_JINDO_MAC")[0] != 'l';
+  for (int l = 0; l < J->p.nq; ++l) J->split_q = J->split_q && (J->p.q[l] >> 60) == 0;
+  for (int l = 0; l < J->p.nqo; ++l) J->split_o = J->split_o && (J->p.qo[l] >> 60) == 0;
+  if (J->split_q) {
+    std::vector<uint64_t> t = J->h_ck_in;
+    split29(t);
+    RG_TRY(J->ck_in_s.upload(t.data(), t.size() * 8));
+    if (!J->h_ck_mlwe.empty()) {
+      t = J->h_ck_mlwe;
+      split29(t);
+      RG_TRY(J->ck_mlwe_s.upload(t.data(), t.size() * 8));
+    }
+  }
+  if (J->split_o) {
+    std::vector<uint64_t> t = J->h_ck_out;
+    split29(t);
+    RG_TRY(J->ck_out_s.upload(t.data(), t.size() * 8));
+  }
   return RG_OK;
 }
 

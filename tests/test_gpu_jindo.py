@@ -60,6 +60,32 @@ def test_commit_matches_oracle(name, nvs):
         assert (com.Value == want["com"]).all(), (name, nv, "Commitment")
 
 
+@pytest.mark.parametrize("name", ["t10_b1", "t14_b1"])
+def test_commit_extreme_noise_matches_oracle(name):
+    """Injected noise far outside the samplers' range (|s| up to 2^63 - 1, INT64_MIN + 1), which
+    takes the encode's term-by-term reduction instead of the one-integer form."""
+    P, q, params = _setup(name)
+    prv = jindo.NewProver(params, b"Jindo!")
+    ck = prv.commit_key()
+    nv = P["rank"]
+    v = make_v(q, nv, seed=3)
+    rnd = make_randomness(P, q, seed=11)
+    rng = np.random.default_rng(12)
+    en = rnd["enc_noise"]
+    ext = np.array([2**63 - 1, -(2**63 - 1), 2**62 + 12345, -(2**61), 2**45 + 1, -(2**44), 2**40, -7],
+                   dtype=np.int64)
+    idx = rng.integers(0, en.size, size=4000)
+    en.reshape(-1)[idx] = ext[rng.integers(0, ext.size, size=idx.size)]
+    mn = rnd["mlwe_noise"]
+    mn.reshape(-1)[rng.integers(0, mn.size, size=500)] = ext[rng.integers(0, ext.size, size=500)]
+    com, op = prv.Commit(v, jindo.Randomness(**rnd))
+    want = _oracle_commit(P, q, ck, v, rnd)
+    assert (op.Encode == want["enc"]).all()
+    assert (op.MLWE == want["mlwe"]).all()
+    assert (op.InCommit == want["incom"]).all()
+    assert (com.Value == want["com"]).all()
+
+
 def test_commit_golden_digests():
     """The jindo_test-size commit against the committed fixture digests."""
     import hashlib
