@@ -600,21 +600,39 @@ static rg_status launch_mac(const MacArgs& m, hipStream_t st) {
   return RG_OK;
 }
 
-// Split-accumulator MAC for primes q < 2^60 (every Jindo ring prime of the configs): with
-// 29-bit low halves a = a0 + a1 2^29 (the commit key is stored pre-split, a0 | a1 << 32) and
-// b = b0 + b1 2^29, a*b = a0b0 + (a0b1 + a1b0) 2^29 + a1b1 2^58, so three 64-bit accumulators
-// absorb `fold` terms (host-computed so no partial sum can wrap) with plain v_mad_u64_u32 (no
-// carries: 4 VALU per MAC instead of ~11) before folding into the exact 128-bit sum.  The sum
-// is the same integer as Acc's, so the reduction and the result are identical.
-// Lanes: lane = jb + nJB * lkl (nJB in {1,2,4,8} output blocks of JB rows share each data word
-// load; 64 / nJB consecutive (limb, coeff) per wave).  The kMac2Waves waves of a workgroup
-// take the SAME (limb, coeff) block and consecutive column groups, so their commit-key loads
-// are the same lines, served by the CU's L1 instead of once per wave from L2.
-constexpr int kMac2Waves = 4;
-struct Mac2Acc {
+// Column-lane MAC for primes q < 2^60 (every Jindo ring prime of the configs).
+// The product is the per-(limb, coeff) modular GEMM out[col][j] = sum_t A[j][t] B[col][t]
+// (prover.go:144-157, 180-191).  A workgroup owns 64 columns (one per lane) x 8 (limb, coeff)
+// (one per wave):
+//  * the commit key is stored split and transposed, As[lk][t][JP] = a0 | a1 << 32 with
+//    a = a0 + a1 2^29, so a wave's slice of a tile (8 terms x JP) is one contiguous 1-KB run;
+//  * B tiles (8 terms x 8 lk x 64 columns, 64-B rows from HBM) and the key slices are staged
+//    through LDS, double-buffered, the next tile's loads in flight during the current tile's
+//    products; key words are wave-uniform LDS reads (broadcast);
+//  * with b = b0 + b1 2^29, a*b = a0b0 + (a0b1 + a1b0) 2^29 + a1b1 2^58: three 64-bit
+//    accumulators absorb `fold` terms with plain v_mad_u64_u32 (4 VALU per MAC, no carries)
+//    before folding into the exact 128-bit sum, the same integer as Acc's, reduced once;
+//  * results are transposed through LDS so every store (and the + MLWE[mlwe + j] read) is a
+//    64-B row.
+constexpr int kMac3Tc = 8;  // terms per LDS tile
+struct Mac3Args {
+  long long per_col, ncols;
+  int J, T1, T2, fold;  // fold: a multiple of kMac3Tc
+  const uint64_t* As;   // [per_col][T1 + T2][JP]
+  const uint64_t* B1;
+  long long b1_col, b1_term;
+  const uint64_t* B2;
+  long long b2_col, b2_term;
+  const uint64_t* C;  // nullable
+  long long c_col, c_j;
+  uint64_t* out;  // [ncols][J][per_col]
+  int d;
+  RnsPrime P[kMaxQ];
+};
+struct Mac3Acc {
   uint64_t s00, s01, s11, lo, hi;
 };
-__device__ __forceinline__ void mac2_fold(Mac2Acc& a) {
+__device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
   uint32_t c0 = 0, c1 = 0, c2 = 0;
   a.lo = addc(a.lo, a.s00, c0);
   a.lo = addc(a.lo, a.s01 << 29, c1);
@@ -623,167 +641,189 @@ __device__ __forceinline__ void mac2_fold(Mac2Acc& a) {
   a.s00 = a.s01 = a.s11 = 0;
 }
 
-template <int JB, int NC>
-__global__ __launch_bounds__(64 * kMac2Waves) void mac2_kernel(MacArgs a, int nJB, int fold) {
-  const long long per_col = (long long)a.nl * a.d;
-  const long long ngroups = (a.ncols + NC - 1) / NC;
-  const int lkw = 64 / nJB;
-  const int lane = (int)(threadIdx.x & 63);
-  const long long wpc = per_col / lkw;  // (limb, coeff) blocks per column group
-  const long long cg = (blockIdx.x / wpc) * kMac2Waves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (cg >= ngroups) return;
-  const long long lkb = blockIdx.x % wpc;
-  const int jb = lane % nJB;
-  const int lk = (int)lkb * lkw + lane / nJB;
-  const int l = lk / a.d;
-  const int j0 = jb * JB;
-  const int J = min(JB, a.J - j0);  // may be <= 0 for padding lanes
-  const long long col0 = cg * NC;
-  const int nc = (int)min((long long)NC, a.ncols - col0);
-  Mac2Acc acc[NC][JB];
+template <int JP>
+__global__ __launch_bounds__(512) void mac3_kernel(Mac3Args a) {
+  static_assert(JP * 8 * 64 <= 2 * kMac3Tc * 8 * 64, "output stage must fit the tile buffers");
+  __shared__ uint64_t lds[2 * kMac3Tc * 8 * 64];  // two B tiles [tt][lk8][col]; then the output stage
+  __shared__ uint64_t lda[2][8][kMac3Tc * JP];     // two key tiles [w][tt][j]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long nlkg = a.per_col / 8;
+  const long long lk0 = (blockIdx.x % nlkg) * 8, c0 = (blockIdx.x / nlkg) * 64;
+  const int lk = (int)lk0 + w;
+  const int T = a.T1 + a.T2;
+  // loader role: column c0 + lane, term tb + w, 8 consecutive lk (64 B)
+  const long long lcol = c0 + lane;
+  const bool lval = lcol < a.ncols;
+  auto gload = [&](int tb, ulonglong2 (&v)[4]) {
+    const int t = tb + w;
+    if (lval && t < T) {
+      const uint64_t* p = t < a.T1 ? a.B1 + lcol * a.b1_col + (long long)t * a.b1_term + lk0
+                                   : a.B2 + lcol * a.b2_col + (long long)(t - a.T1) * a.b2_term + lk0;
+      const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
 #pragma unroll
-  for (int c = 0; c < NC; ++c)
+      for (int i = 0; i < 4; ++i) v[i] = q[i];
+    } else {
 #pragma unroll
-    for (int j = 0; j < JB; ++j) acc[c][j] = Mac2Acc{0, 0, 0, 0, 0};
-  for (int set = 0; set < 2; ++set) {
-    const int T = set ? a.T2 : a.T1;
-    if (!T) continue;
-    // buffer addressing: per-lane offsets, per-term strides in SGPRs; the next term's words
-    // are loaded while the current term is multiplied (one term of prefetch)
-    const __amdgpu_buffer_rsrc_t ra = rg_buf(set ? a.A2 : a.A1);
-    const uint32_t astride = (uint32_t)(per_col * 8);
-    const long long bcol = set ? a.b2_col : a.b1_col, bterm = set ? a.b2_term : a.b1_term;
-    const uint64_t* Bb = set ? a.B2 : a.B1;
-    __amdgpu_buffer_rsrc_t rb[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {  // wave-uniform base, so the resource lives in SGPRs
-      const uint64_t pb = (uint64_t)(Bb + (col0 + (c < nc ? c : 0)) * bcol);
-      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
-      rb[c] = rg_buf((const void*)(((uint64_t)hi << 32) | lo));
+      for (int i = 0; i < 4; ++i) v[i] = make_ulonglong2(0, 0);
     }
-    const uint32_t bvo = (uint32_t)lk * 8u, bstride = (uint32_t)(bterm * 8);
-    // padding rows (j >= J) and columns (c >= nc) load valid words and are never stored, so
-    // every load is unconditional
-    uint32_t avj[JB];
+  };
+  auto lstore = [&](int buf, const ulonglong2 (&v)[4]) {
+    uint64_t* L = lds + buf * (kMac3Tc * 8 * 64) + (w * 8) * 64 + lane;
 #pragma unroll
-    for (int j = 0; j < JB; ++j) avj[j] = (uint32_t)(((long long)min(j0 + j, a.J - 1) * T * per_col + lk) * 8);
-    auto load = [&](int t, uint64_t (&x)[JB], uint64_t (&y)[NC]) {
-#pragma unroll
-      for (int j = 0; j < JB; ++j) x[j] = rg_bload(ra, avj[j], (uint32_t)t * astride);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) y[c] = rg_bload(rb[c], bvo, (uint32_t)t * bstride);
-    };
-    auto madd = [&](const uint64_t (&x)[JB], const uint64_t (&y)[NC]) {
-      uint32_t b0[NC], b1[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        b0[c] = (uint32_t)y[c] & 0x1fffffffu;
-        b1[c] = (uint32_t)(y[c] >> 29);
-      }
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          const uint32_t a0 = (uint32_t)x[j], a1 = (uint32_t)(x[j] >> 32);
-          Mac2Acc& z = acc[c][j];
-          z.s00 = mad64(a0, b0[c], z.s00);
-          z.s01 = mad64(a0, b1[c], z.s01);
-          z.s01 = mad64(a1, b0[c], z.s01);
-          z.s11 = mad64(a1, b1[c], z.s11);
-        }
-    };
-    for (int t0 = 0; t0 < T; t0 += fold) {
-      const int t1 = min(T, t0 + fold);
-      int t = t0;
-      // two terms per trip, ping-pong buffers: the loads of term t+1 are in flight while term t
-      // is multiplied, with no register copies
-      uint64_t xa[JB], ya[NC], xb[JB], yb[NC];
-      load(t, xa, ya);
-      for (; t + 1 < t1; t += 2) {
-        load(t + 1, xb, yb);
-        madd(xa, ya);
-        if (t + 2 < t1) load(t + 2, xa, ya);
-        madd(xb, yb);
-      }
-      if (t < t1) madd(xa, ya);
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int j = 0; j < JB; ++j) mac2_fold(acc[c][j]);
+    for (int i = 0; i < 4; ++i) {
+      L[(2 * i) * 64] = v[i].x;
+      L[(2 * i + 1) * 64] = v[i].y;
     }
+  };
+  // key loader role: lane < 4 JP loads 16 B of wave w's slice (8 terms x JP words)
+  const ulonglong2* Aw = reinterpret_cast<const ulonglong2*>(a.As + (long long)lk * T * JP);
+  auto aload = [&](int tb, ulonglong2& v) {
+    const int tt = lane / (JP / 2);
+    v = (lane < 4 * JP && tb + tt < T) ? Aw[(long long)tb * (JP / 2) + lane] : make_ulonglong2(0, 0);
+  };
+  auto astore = [&](int buf, const ulonglong2& v) {
+    if (lane < 4 * JP) reinterpret_cast<ulonglong2*>(lda[buf][w])[lane] = v;
+  };
+  Mac3Acc acc[JP];
+#pragma unroll
+  for (int j = 0; j < JP; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
+  ulonglong2 pre[4], apre;
+  gload(0, pre);
+  aload(0, apre);
+  lstore(0, pre);
+  astore(0, apre);
+  __syncthreads();
+  int buf = 0, since = 0;
+  for (int tb = 0; tb < T; tb += kMac3Tc) {
+    const bool more = tb + kMac3Tc < T;
+    if (more) {
+      gload(tb + kMac3Tc, pre);
+      aload(tb + kMac3Tc, apre);
+    }
+    const uint64_t* L = lds + buf * (kMac3Tc * 8 * 64) + w * 64 + lane;
+    const uint64_t* LA = lda[buf][w];
+#pragma unroll
+    for (int tt = 0; tt < kMac3Tc; ++tt) {
+      const int t = tb + tt;
+      if (t >= T) break;
+      const uint64_t b = L[tt * 8 * 64];
+      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29);
+#pragma unroll
+      for (int j = 0; j < JP; ++j) {
+        const uint64_t av = LA[tt * JP + j];
+        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32);
+        Mac3Acc& z = acc[j];
+        z.s00 = mad64(a0, b0, z.s00);
+        z.s01 = mad64(a0, b1, z.s01);
+        z.s01 = mad64(a1, b0, z.s01);
+        z.s11 = mad64(a1, b1, z.s11);
+      }
+    }
+    since += kMac3Tc;
+    if (since >= a.fold) {
+#pragma unroll
+      for (int j = 0; j < JP; ++j) mac3_fold(acc[j]);
+      since = 0;
+    }
+    if (more) {
+      lstore(buf ^ 1, pre);
+      astore(buf ^ 1, apre);
+    }
+    __syncthreads();
+    buf ^= 1;
   }
-  const RnsPrime& P = a.P[l];
+  // reduce: (lo + hi 2^64) 2^-64 mod q = lo 2^-64 + hi (MulCoeffsMontgomeryThenAdd summed)
+  const RnsPrime& P = a.P[lk / a.d];
+  const uint64_t q = P.q;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (c >= nc) continue;
-    const long long col = col0 + c;
+  for (int j = 0; j < JP; ++j) {
+    mac3_fold(acc[j]);
+    uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
+    r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
+    lds[(j * 8 + w) * 64 + lane] = r;  // [j][lk8][col]
+  }
+  __syncthreads();
+  // store: (col, j) pairs, 8 consecutive lk = one 64-B row each
+  for (int pidx = tid; pidx < JP * 64; pidx += 512) {
+    const int c = pidx & 63, j = pidx >> 6;
+    const long long col = c0 + c;
+    if (j >= a.J || col >= a.ncols) continue;
+    uint64_t r[8];
 #pragma unroll
-    for (int j = 0; j < JB; ++j) {
-      if (j >= J) continue;
-      const uint64_t q = P.q;
-      uint64_t r = sh_mul(acc[c][j].lo, P.rinv, P.rinv_sh, q);
-      r = mod_add(r, sh_mul(acc[c][j].hi, 1, P.one_sh, q), q);
-      if (a.C) r = mod_add(a.C[col * a.c_col + (long long)(j0 + j) * a.c_j + lk], r, P.q);
-      a.out[(col * a.J + j0 + j) * per_col + lk] = r;
+    for (int x = 0; x < 8; ++x) r[x] = lds[(j * 8 + x) * 64 + c];
+    if (a.C) {
+      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const ulonglong2 cv = cp[i];
+        const uint64_t qa = a.P[(int)((lk0 + 2 * i) / a.d)].q;  // 8 lk never straddle a limb (d % 8 == 0)
+        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
+        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
+      }
     }
+    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
   }
 }
 
-constexpr int kMac2NC = 2;
-template <int JB>
-static rg_status launch_mac2_jb(const MacArgs& m, int nJB, int fold, hipStream_t st) {
-  const long long groups = (m.ncols + kMac2NC - 1) / kMac2NC;
-  const long long wpc = (long long)(m.nl * m.d) / (64 / nJB);
-  const long long blocks = (groups + kMac2Waves - 1) / kMac2Waves * wpc;
-  hipLaunchKernelGGL((mac2_kernel<JB, kMac2NC>), dim3((unsigned)blocks), dim3(64 * kMac2Waves), 0, st, m, nJB, fold);
-  return check_launch("jindo mac2");
+// J padded to the instantiated widths
+static int mac3_jp(int J) {
+  static const int w[] = {4, 6, 8, 10, 12, 16};
+  for (int x : w)
+    if (J <= x) return x;
+  return 0;
 }
 
 // fold period: the largest F <= 32 with F * max partial product < 2^64 in every accumulator
-// (a0 b0 < 2^58, two of a0 b1, a1 b0 < 2^bits per term, a1 b1 < 2^(2 (bits - 29)))
-static int mac2_fold(const MacArgs& m) {
+// (a0 b0 < 2^58, two of a0 b1, a1 b0 < 2^bits per term, a1 b1 < 2^(2 (bits - 29))),
+// rounded down to whole tiles
+static int mac3_fold_period(const RnsPrime* P, int nl) {
   int bits = 29;
-  for (int l = 0; l < m.nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(m.P[l].q - 1));
+  for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
   int f = 32;
   while (f > 1 && ((double)f * 2.0 * std::ldexp(1.0, bits) > std::ldexp(1.0, 64) ||
                    (double)f * std::ldexp(1.0, 2 * std::max(0, bits - 29)) > std::ldexp(1.0, 64)))
     f >>= 1;
-  return f;
+  return f & ~(kMac3Tc - 1);
 }
 
-// eligible: primes < 2^60 with a fold period >= 4, the sum fits 128 bits, and 64 (limb, coeff)
-// lanes tile a column
-static bool mac2_ok(const MacArgs& m) {
-  for (int l = 0; l < m.nl; ++l)
-    if (m.P[l].q >> 60) return false;
+// eligible: a fold period of at least one tile, J <= 16, the exact sum below 2^128, 8 | d
+static bool mac3_ok(const RnsPrime* P, int nl, int J, int T, int d) {
   int bits = 0;
-  for (int l = 0; l < m.nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(m.P[l].q - 1));
-  const bool fits128 = (double)(m.T1 + m.T2) * std::ldexp(1.0, 2 * bits) < std::ldexp(1.0, 128);
-  // measured: ahead of mac_kernel at J <= 10 (one shared data load per 2 lanes); at J = 16 the
-  // 4-lane sharing makes it load-issue bound and slower than mac_kernel
-  return mac2_fold(m) >= 4 && fits128 && (m.nl * m.d) % 64 == 0 && m.J <= 10;
+  for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
+  const bool fits128 = (double)T * std::ldexp(1.0, 2 * bits) < std::ldexp(1.0, 128);
+  return mac3_fold_period(P, nl) >= kMac3Tc && mac3_jp(J) > 0 && fits128 && d % 8 == 0;
 }
 
-static rg_status launch_mac2(const MacArgs& m, hipStream_t st) {
-  const int fold = mac2_fold(m);
-  static const int maxjb = [] {  // RINGO_JINDO_MAC2_JB: outputs per lane (tuning)
-    const char* e = getenv("RINGO_JINDO_MAC2_JB");
-    return e ? std::max(1, std::min(5, atoi(e))) : 5;
-  }();
-  int nJB = 1;
-  while (nJB < 8 && (m.J + nJB - 1) / nJB > maxjb) nJB *= 2;
-  switch ((m.J + nJB - 1) / nJB) {
-    case 1: return launch_mac2_jb<1>(m, nJB, fold, st);
-    case 2: return launch_mac2_jb<2>(m, nJB, fold, st);
-    case 3: return launch_mac2_jb<3>(m, nJB, fold, st);
-    case 4: return launch_mac2_jb<4>(m, nJB, fold, st);
-    default: return launch_mac2_jb<5>(m, nJB, fold, st);
+static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
+  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
+  const dim3 g((unsigned)blocks), b(512);
+  switch (mac3_jp(m.J)) {
+    case 4: hipLaunchKernelGGL(mac3_kernel<4>, g, b, 0, st, m); break;
+    case 6: hipLaunchKernelGGL(mac3_kernel<6>, g, b, 0, st, m); break;
+    case 8: hipLaunchKernelGGL(mac3_kernel<8>, g, b, 0, st, m); break;
+    case 10: hipLaunchKernelGGL(mac3_kernel<10>, g, b, 0, st, m); break;
+    case 12: hipLaunchKernelGGL(mac3_kernel<12>, g, b, 0, st, m); break;
+    default: hipLaunchKernelGGL(mac3_kernel<16>, g, b, 0, st, m); break;
   }
+  return check_launch("jindo mac3");
 }
 
-// host: the commit key in split form (a & (2^29 - 1)) | (a >> 29) << 32
-static void split29(std::vector<uint64_t>& v) {
-  for (auto& x : v) x = (x & 0x1fffffffull) | ((x >> 29) << 32);
+// host: the commit key of one MAC, split and transposed for mac3_kernel:
+// out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J zero)
+static std::vector<uint64_t> mac3_key(const std::vector<uint64_t>& A1, int T1, const std::vector<uint64_t>& A2,
+                                      int T2, int J, size_t per_col) {
+  const int JP = mac3_jp(J), T = T1 + T2;
+  std::vector<uint64_t> o(per_col * T * JP, 0);
+  for (size_t lk = 0; lk < per_col; ++lk)
+    for (int t = 0; t < T; ++t)
+      for (int j = 0; j < J; ++j) {
+        const uint64_t x = t < T1 ? A1[((size_t)j * T1 + t) * per_col + lk] : A2[((size_t)j * T2 + (t - T1)) * per_col + lk];
+        o[(lk * T + t) * JP + j] = (x & 0x1fffffffull) | ((x >> 29) << 32);
+      }
+  return o;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -921,8 +961,8 @@ struct rg_jindo {
   rg::DstDev dst_o;
   std::vector<uint64_t> h_ck_in, h_ck_mlwe, h_ck_out;
   rg::DevBuf ck_in, ck_mlwe, ck_out;
-  rg::DevBuf ck_in_s, ck_mlwe_s, ck_out_s;  // 29-bit split copies for mac2_kernel (primes < 2^60)
-  bool split_q = false, split_o = false;
+  rg::DevBuf ck3_in, ck3_out;  // commit keys split + transposed for mac3_kernel (inner, outer)
+  bool mac3_q = false, mac3_o = false;
   uint64_t base_inv;
   std::mutex mu;  // guards the scratch cache
   rg::DevBuf s_digits, s_com, s_ocom, s_skip;
@@ -1182,6 +1222,32 @@ static bool prep_legacy() {
   return v == 1;
 }
 
+// MacArgs (legacy kernel layout) -> Mac3Args
+static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
+  Mac3Args a;
+  memset(&a, 0, sizeof(a));
+  a.per_col = (long long)m.nl * m.d;
+  a.ncols = m.ncols;
+  a.J = m.J;
+  a.T1 = m.T1;
+  a.T2 = m.T2;
+  a.fold = fold;
+  a.As = As;
+  a.B1 = m.B1;
+  a.b1_col = m.b1_col;
+  a.b1_term = m.b1_term;
+  a.B2 = m.B2;
+  a.b2_col = m.b2_col;
+  a.b2_term = m.b2_term;
+  a.C = m.C;
+  a.c_col = m.c_col;
+  a.c_j = m.c_j;
+  a.out = m.out;
+  a.d = m.d;
+  for (int l = 0; l < m.nl; ++l) a.P[l] = m.P[l];
+  return a;
+}
+
 static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
                             const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
                             uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
@@ -1258,10 +1324,8 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   ma.c_j = (long long)nq * d;
   ma.out = J->s_com.as<uint64_t>();
   for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
-  if (J->split_q && mac2_ok(ma)) {
-    ma.A1 = J->ck_in_s.as<uint64_t>();
-    ma.A2 = J->ck_mlwe_s.as<uint64_t>();
-    RG_TRY(launch_mac2(ma, st));
+  if (J->mac3_q) {
+    RG_TRY(launch_mac3(mac3_args(ma, J->ck3_in.as<uint64_t>(), mac3_fold_period(J->rq, nq)), st));
   } else {
     RG_TRY(launch_mac(ma, st));
   }
@@ -1297,9 +1361,8 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   mo.b1_term = (long long)nqo * d;
   mo.out = J->s_ocom.as<uint64_t>();
   for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
-  if (J->split_o && mac2_ok(mo)) {
-    mo.A1 = J->ck_out_s.as<uint64_t>();
-    RG_TRY(launch_mac2(mo, st));
+  if (J->mac3_o) {
+    RG_TRY(launch_mac3(mac3_args(mo, J->ck3_out.as<uint64_t>(), mac3_fold_period(J->ro, nqo)), st));
   } else {
     RG_TRY(launch_mac(mo, st));
   }
@@ -1340,23 +1403,18 @@ static rg_status upload_ck(rg_jindo* J) {
   RG_TRY(J->ck_in.upload(J->h_ck_in.data(), J->h_ck_in.size() * 8));
   if (!J->h_ck_mlwe.empty()) RG_TRY(J->ck_mlwe.upload(J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8));
   RG_TRY(J->ck_out.upload(J->h_ck_out.data(), J->h_ck_out.size() * 8));
-  J->split_q = J->split_o = getenv("RINGO_JINDO_MAC") == nullptr || getenv("RINGO_JINDO_MAC")[0] != 'l';
-  for (int l = 0; l < J->p.nq; ++l) J->split_q = J->split_q && (J->p.q[l] >> 60) == 0;
-  for (int l = 0; l < J->p.nqo; ++l) J->split_o = J->split_o && (J->p.qo[l] >> 60) == 0;
-  if (J->split_q) {
-    std::vector<uint64_t> t = J->h_ck_in;
-    split29(t);
-    RG_TRY(J->ck_in_s.upload(t.data(), t.size() * 8));
-    if (!J->h_ck_mlwe.empty()) {
-      t = J->h_ck_mlwe;
-      split29(t);
-      RG_TRY(J->ck_mlwe_s.upload(t.data(), t.size() * 8));
-    }
+  const rg_jindo_params& p = J->p;
+  const bool legacy = getenv("RINGO_JINDO_MAC") && getenv("RINGO_JINDO_MAC")[0] == 'l';  // A/B switch
+  const size_t pcq = (size_t)p.nq * p.d, pco = (size_t)p.nqo * p.d;
+  J->mac3_q = !legacy && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
+  J->mac3_o = !legacy && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
+  if (J->mac3_q) {
+    const std::vector<uint64_t> t = mac3_key(J->h_ck_in, p.rows, J->h_ck_mlwe, p.mlwe, p.in_msis, pcq);
+    RG_TRY(J->ck3_in.upload(t.data(), t.size() * 8));
   }
-  if (J->split_o) {
-    std::vector<uint64_t> t = J->h_ck_out;
-    split29(t);
-    RG_TRY(J->ck_out_s.upload(t.data(), t.size() * 8));
+  if (J->mac3_o) {
+    const std::vector<uint64_t> t = mac3_key(J->h_ck_out, p.dcmp, {}, 0, p.out_msis, pco);
+    RG_TRY(J->ck3_out.upload(t.data(), t.size() * 8));
   }
   return RG_OK;
 }
