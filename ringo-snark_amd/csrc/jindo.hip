@@ -316,8 +316,8 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("" ::: "memory");
 }
 template <int RK, int LO, int PAT>
-__device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, uint64_t q, uint64_t q2,
-                                           uint32_t t) {
+__device__ __forceinline__ void prep_round(uint64_t (&e)[8], __amdgpu_buffer_rsrc_t roots, uint32_t rbase, uint64_t q,
+                                           uint64_t q2, uint32_t t) {
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
@@ -331,7 +331,8 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
     for (int j = 0; j < 4; ++j) {
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
-      const ulonglong2 w = roots[(1u << k) + (xof(rho0) >> (b + 1))];
+      const rg_u32x4 wv = __builtin_amdgcn_raw_buffer_load_b128(roots, rbase + ((1u << k) + (xof(rho0) >> (b + 1))) * 16u, 0, 0);
+      const ulonglong2 w = make_ulonglong2(pk(wv.x, wv.y), pk(wv.z, wv.w));
       // Harvey: values in [0, 4q) (ring primes are < 2^62), twiddle product in [0, 2q)
       uint64_t x = e[rho0];
       x = x >= q2 ? x - q2 : x;
@@ -349,7 +350,8 @@ __device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
   return c < 0 ? mod_neg(m, P.q) : m;
 }
 
-__global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
+template <int MINW>
+__global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs a) {
   __shared__ uint64_t lds_all[kPrepWaves][2 * 288];
   const JShape& S = a.s;
   const int nq = S.nq;
@@ -376,26 +378,6 @@ __global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
     dst = a.mlwe + mj * nq * 256;
     nz = a.mlwe_noise + mj * 256;
   }
-  // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
-  // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
-  // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  v is limb independent.
-  long long v[8];
-  uint32_t big = 0;  // bit y: coefficient t + 32 y needs the term-by-term form
-#pragma unroll
-  for (int y = 0; y < 8; ++y) {
-    const int k = (int)t + 32 * y;
-    const long long c = nz[k];
-    if (is_enc) {
-      const int ks = k - S.slots;
-      const long long cs = ks >= 0 ? nz[ks] : nz[ks + 256];
-      const uint64_t s2 = k < S.slots ? 0ull - (uint64_t)cs : (uint64_t)cs;  // wrapped coefficients negate
-      const bool ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
-      big |= ok ? 0u : (1u << y);
-      v[y] = (long long)((uint64_t)dg[k] + s2 - (uint64_t)c * S.base);
-    } else {
-      v[y] = c;
-    }
-  }
   const uint32_t rH = 288 * hs + t, rM = 288 * hs + 36 * (t >> 2) + (t & 3), rL9 = 288 * hs + 9 * t,
                  rL8 = 288 * hs + 8 * t + (t >> 2);
   for (int l0 = 0; l0 < nq; l0 += 2) {
@@ -404,14 +386,30 @@ __global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
     const int lc = active ? limb : l0;
     const RnsPrime& P = a.R.p[lc];
     const uint64_t q = P.q, q2 = 2 * q;
-    const ulonglong2* roots = a.R.fwd + (long long)lc * 256;
+    const __amdgpu_buffer_rsrc_t roots = rg_buf(a.R.fwd);  // uniform; the limb is a lane offset
+    const uint32_t rbase = (uint32_t)lc * 256u * 16u;
+    // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
+    // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
+    // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  Inputs are (re)read per
+    // limb pair rather than held across the NTT.
     uint64_t e[8];
+    uint32_t big = 0;  // bit y: coefficient t + 32 y needs the term-by-term form
 #pragma unroll
     for (int y = 0; y < 8; ++y) {
-      const long long vy = v[y];
-      const uint64_t av = vy < 0 ? (uint64_t)(-(vy + 1)) + 1 : (uint64_t)vy;
+      const int k = (int)t + 32 * y;
+      const long long c = nz[k];
+      long long v = c;
+      if (is_enc) {
+        const int ks = k - S.slots;
+        const long long cs = ks >= 0 ? nz[ks] : nz[ks + 256];
+        const uint64_t s2 = k < S.slots ? 0ull - (uint64_t)cs : (uint64_t)cs;  // wrapped coefficients negate
+        const bool ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
+        big |= ok ? 0u : (1u << y);
+        v = (long long)((uint64_t)dg[k] + s2 - (uint64_t)c * S.base);
+      }
+      const uint64_t av = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
       const uint64_t m = sh_mul(av, P.r64, P.r64_sh, q);  // Shoup: exact for any 64-bit input
-      e[y] = vy < 0 ? mod_neg(m, q) : m;
+      e[y] = v < 0 ? mod_neg(m, q) : m;
     }
     if (big) {  // rare (huge injected noise): every term reduced separately, same residue
       for (int y = 0; y < 8; ++y) {
@@ -426,20 +424,20 @@ __global__ __launch_bounds__(64 * kPrepWaves) void prep256_kernel(PrepArgs a) {
       }
     }
     // NTT: H round (stages 0-2), H->M, M round (3-5), M->L, L round (6-7), L->H, store
-    prep_round<3, 5, 0>(e, roots, q, q2, t);
+    prep_round<3, 5, 0>(e, roots, rbase, q, q2, t);
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[rM + 4 * y];
-    prep_round<3, 2, 1>(e, roots, q, q2, t);
+    prep_round<3, 2, 1>(e, roots, rbase, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rM + 4 * y + (y >> 1)] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[rL9 + r];
-    prep_round<2, 0, 2>(e, roots, q, q2, t);
+    prep_round<2, 0, 2>(e, roots, rbase, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) {  // [0, 4q) -> [0, q)
@@ -1296,11 +1294,21 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   const long long n_ml = (long long)batch * (p.cols + 1) * nm;
   pa.n_ml = n_ml;
   pa.clim = (long long)(((uint64_t)1 << 61) / p.base);
-  if (d == 256 && !prep_legacy())
-    hipLaunchKernelGGL(prep256_kernel, dim3((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)),
-                       dim3(64 * kPrepWaves), 0, st, pa);
-  else
+  if (d == 256 && !prep_legacy()) {
+    static const int pw = [] {  // RINGO_JINDO_PREP_W: minimum waves per SIMD for prep256 (tuning)
+      const char* e = getenv("RINGO_JINDO_PREP_W");
+      return e ? atoi(e) : 6;
+    }();
+    const dim3 g((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
+    if (pw >= 8)
+      hipLaunchKernelGGL(prep256_kernel<8>, g, b, 0, st, pa);
+    else if (pw >= 6)
+      hipLaunchKernelGGL(prep256_kernel<6>, g, b, 0, st, pa);
+    else
+      hipLaunchKernelGGL(prep256_kernel<1>, g, b, 0, st, pa);
+  } else {
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
+  }
   RG_TRY(check_launch("jindo prep"));
   // 3. inner MAC
   MacArgs ma;
