@@ -135,6 +135,7 @@ struct DigitArgs {
   JShape s;
   FieldParams<L> F;
   uint64_t base_inv;  // floor(2^64 / base)
+  uint64_t b2, b2_inv;  // base^2 and floor(2^64 / base^2) when base^2 < 2^32, else 0
   const uint64_t* v;         // [B][nv][L]
   const uint64_t* last_row;  // [B][cols*slots][L]
   const uint64_t* mask;      // [B][rows][slots][L]
@@ -216,7 +217,30 @@ __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
     w[2 * l] = (uint32_t)c[l];
     w[2 * l + 1] = (uint32_t)(c[l] >> 32);
   }
-  for (int jd = 0; jd < S.exp - 1; ++jd) {
+  int jd = 0;
+  if (a.b2) {  // two digits per long division: divide by b^2 (< 2^32), split the remainder
+    // words above `top` are zero (the value shrinks ~2 log2(b) bits a pass); the word loop stays
+    // unrolled with a predicate so w[] is never indexed dynamically (registers, not scratch)
+    auto top_of = [&]() {
+      int tp = 0;
+#pragma unroll
+      for (int k = 1; k < 2 * L; ++k) tp = w[k] ? k : tp;
+      return tp;
+    };
+    int top = top_of();
+    for (; jd + 1 < S.exp - 1; jd += 2) {
+      uint64_t rem = 0;
+#pragma unroll
+      for (int k = 2 * L - 1; k >= 0; --k)
+        if (k <= top) w[k] = divstep((rem << 32) | w[k], a.b2, a.b2_inv, rem);
+      top = top_of();
+      uint64_t lo;
+      const uint32_t hi = divstep(rem, S.base, a.base_inv, lo);
+      out[jd * S.slots + slot] = (uint32_t)lo;
+      out[(jd + 1) * S.slots + slot] = hi;
+    }
+  }
+  for (; jd < S.exp - 1; ++jd) {
     uint64_t rem = 0;
 #pragma unroll
     for (int k = 2 * L - 1; k >= 0; --k) w[k] = divstep((rem << 32) | w[k], S.base, a.base_inv, rem);
@@ -1190,6 +1214,9 @@ static rg_status launch_digits(const rg_jindo* J, size_t batch, const uint64_t* 
   memcpy(a.F.q, J->field.q, 8 * L);
   a.F.qinv = J->field.qinv;
   a.base_inv = J->base_inv;
+  const uint64_t b2 = (uint64_t)J->p.base * J->p.base;
+  a.b2 = (b2 >> 32) ? 0 : b2;
+  a.b2_inv = a.b2 ? (uint64_t)(((unsigned __int128)1 << 64) / b2) : 0;
   a.v = v;
   a.last_row = last;
   a.mask = mask;
