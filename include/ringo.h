@@ -173,6 +173,30 @@ rg_status rg_jindo_commit_dev(const rg_jindo* j, size_t batch, const uint64_t* d
  * cached inside the handle on first use; exposed for capacity planning). */
 size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
 
+/* Prover.Evaluate (prover.go:205-324), device-resident, with the Fiat-Shamir challenges
+ * INJECTED: the transcript (SHAKE128 over CommitKey/Commitment/Proof serializations),
+ * encodeChallengeTo, leftVec/encode and Poly.Evaluate stay in the Go caller, which also keeps
+ * the shape panics (:206-216).  Challenge polynomials are ringQ / ringQOut residues in the
+ * NTT + Montgomery domain, as Go holds them; every product is MulCoeffsMontgomeryThenAdd.
+ * 1. openBatch = sum_i open[i] * batch[i] (:228-266), or open[0] when batch == 1 (:267-269):
+ *      d_incom [batch][dcmp][nqo][d], d_enc [batch][cols+1][rows][nq][d],
+ *      d_mlwe [batch][cols+1][in_msis+mlwe][nq][d]  the openings (rg_jindo_commit_dev layout)
+ *      d_bq [batch][nq][d], d_bo [batch][nqo][d]     batch[i] in ringQ and batchOut[i] in ringQOut
+ *      d_ob_*  openBatch in the single-opening layouts; openBatch.InCommit = Proof.InCommit */
+rg_status rg_jindo_eval_batch_dev(const rg_jindo* j, size_t batch, const uint64_t* d_incom, const uint64_t* d_enc,
+                                  const uint64_t* d_mlwe, const uint64_t* d_bq, const uint64_t* d_bo,
+                                  uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe, void* stream);
+/* 2. Proof.Partial[i] = sum_j left[j] * openBatch.Encode[i][j] (:274-278) and
+ *    Proof.PartialMask over column cols (:280-282):
+ *      d_left [rows][nq][d] (encode(leftVec(x)[j]))   d_partial [cols+1][nq][d], last = PartialMask */
+rg_status rg_jindo_eval_partial_dev(const rg_jindo* j, const uint64_t* d_ob_enc, const uint64_t* d_left,
+                                    uint64_t* d_partial, void* stream);
+/* 3. Proof.Encode[i] = openBatch.Encode[cols][i] + sum_j chals[j] * openBatch.Encode[j][i] and
+ *    Proof.MLWE[i] likewise (:300-314):
+ *      d_chals [cols][nq][d]   d_pf_enc [rows][nq][d]   d_pf_mlwe [in_msis+mlwe][nq][d]          */
+rg_status rg_jindo_eval_respond_dev(const rg_jindo* j, const uint64_t* d_ob_enc, const uint64_t* d_ob_mlwe,
+                                    const uint64_t* d_chals, uint64_t* d_pf_enc, uint64_t* d_pf_mlwe, void* stream);
+
 /* ------------------------------------------------------------------------------------ */
 /* Device memory helpers (so a cgo caller needs no HIP headers)                           */
 /* ------------------------------------------------------------------------------------ */

@@ -32,6 +32,9 @@ def lib():
         L.of_ntt_fwd.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
         L.of_ntt_inv.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
         L.of_vec.argtypes = [ctypes.c_void_p, ctypes.c_int, u64p, u64p, u64p, ctypes.c_long]
+        L.of_jindo_eval_batch.argtypes = [ctypes.c_void_p, ctypes.c_long] + [u64p] * 8
+        L.of_jindo_eval_partial.argtypes = [ctypes.c_void_p, u64p, u64p, u64p]
+        L.of_jindo_eval_respond.argtypes = [ctypes.c_void_p] + [u64p] * 5
     return _LIB
 
 
@@ -197,3 +200,33 @@ class CJindo:
         if rc:
             raise ValueError("len(v) > params.rank")
         return o
+
+    # ---- Prover.Evaluate core (prover.go:205-324), challenges injected ----
+    def eval_shapes(self):
+        s = self.ps
+        nm = s.in_msis + s.mlwe
+        return dict(ob_incom=(s.dcmp, s.nqo, s.d), ob_enc=(s.cols + 1, s.rows, s.nq, s.d),
+                    ob_mlwe=(s.cols + 1, nm, s.nq, s.d), partial=(s.cols + 1, s.nq, s.d),
+                    pf_enc=(s.rows, s.nq, s.d), pf_mlwe=(nm, s.nq, s.d))
+
+    def eval_batch(self, incom, enc, mlwe, bq, bo):
+        """openBatch = sum_i open[i] * batch[i]; inputs carry a leading batch dimension."""
+        sh = self.eval_shapes()
+        o = {k: np.zeros(sh[k], np.uint64) for k in ("ob_incom", "ob_enc", "ob_mlwe")}
+        a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (incom, enc, mlwe, bq, bo)]
+        lib().of_jindo_eval_batch(ctypes.c_void_p(self.h), ctypes.c_long(a[0].shape[0]), *[ptr(x) for x in a],
+                                  ptr(o["ob_incom"]), ptr(o["ob_enc"]), ptr(o["ob_mlwe"]))
+        return o
+
+    def eval_partial(self, ob_enc, left):
+        out = np.zeros(self.eval_shapes()["partial"], np.uint64)
+        a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (ob_enc, left)]
+        lib().of_jindo_eval_partial(ctypes.c_void_p(self.h), ptr(a[0]), ptr(a[1]), ptr(out))
+        return out
+
+    def eval_respond(self, ob_enc, ob_mlwe, chals):
+        sh = self.eval_shapes()
+        pe, pm = np.zeros(sh["pf_enc"], np.uint64), np.zeros(sh["pf_mlwe"], np.uint64)
+        a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (ob_enc, ob_mlwe, chals)]
+        lib().of_jindo_eval_respond(ctypes.c_void_p(self.h), ptr(a[0]), ptr(a[1]), ptr(a[2]), ptr(pe), ptr(pm))
+        return pe, pm

@@ -771,3 +771,78 @@ int of_jindo_commit(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck
   free(first);
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Prover.Evaluate core (jindo/prover.go:205-324) with the Fiat-Shamir challenges injected:   */
+/* the transcript (SHAKE128 over Lattigo serializations), encodeChallengeTo and leftVec stay  */
+/* on the host; these are the MulCoeffsMontgomeryThenAdd loops.  Layouts: include/ringo.h.   */
+/* ------------------------------------------------------------------------------------------ */
+/* openBatch = sum_i open[i] * batch[i] (prover.go:228-266); batch == 1: open[0] (:267-269) */
+void of_jindo_eval_batch(const of_jindo* J, long batch, const uint64_t* incom, const uint64_t* enc,
+                         const uint64_t* mlwe, const uint64_t* bq, const uint64_t* bo, uint64_t* ob_incom,
+                         uint64_t* ob_enc, uint64_t* ob_mlwe) {
+  const of_jindo_params* P = &J->P;
+  const int d = P->d, nq = P->nq, nqo = P->nqo, nm = P->in_msis + P->mlwe;
+  const size_t polyq = (size_t)nq * d, polyo = (size_t)nqo * d;
+  const size_t n_inc = (size_t)P->dcmp, n_enc = (size_t)(P->cols + 1) * P->rows, n_ml = (size_t)(P->cols + 1) * nm;
+  if (batch == 1) {
+    memcpy(ob_incom, incom, 8 * n_inc * polyo);
+    memcpy(ob_enc, enc, 8 * n_enc * polyq);
+    memcpy(ob_mlwe, mlwe, 8 * n_ml * polyq);
+    return;
+  }
+  memset(ob_incom, 0, 8 * n_inc * polyo);
+  memset(ob_enc, 0, 8 * n_enc * polyq);
+  memset(ob_mlwe, 0, 8 * n_ml * polyq);
+  for (long i = 0; i < batch; ++i) {
+    for (size_t j = 0; j < n_inc; ++j)
+      for (int l = 0; l < nqo; ++l)
+        mac_mont(ob_incom + j * polyo + (size_t)l * d, incom + ((size_t)i * n_inc + j) * polyo + (size_t)l * d,
+                 bo + (size_t)i * polyo + (size_t)l * d, &J->ro[l], d);
+    for (size_t j = 0; j < n_enc; ++j)
+      for (int l = 0; l < nq; ++l)
+        mac_mont(ob_enc + j * polyq + (size_t)l * d, enc + ((size_t)i * n_enc + j) * polyq + (size_t)l * d,
+                 bq + (size_t)i * polyq + (size_t)l * d, &J->rq[l], d);
+    for (size_t j = 0; j < n_ml; ++j)
+      for (int l = 0; l < nq; ++l)
+        mac_mont(ob_mlwe + j * polyq + (size_t)l * d, mlwe + ((size_t)i * n_ml + j) * polyq + (size_t)l * d,
+                 bq + (size_t)i * polyq + (size_t)l * d, &J->rq[l], d);
+  }
+}
+
+/* pf.Partial[i] = sum_j left[j] * Enc[i][j] (i < cols), PartialMask the same over column cols
+   (prover.go:274-286); partial: [cols+1][nq][d], the last polynomial is PartialMask */
+void of_jindo_eval_partial(const of_jindo* J, const uint64_t* ob_enc, const uint64_t* left, uint64_t* partial) {
+  const of_jindo_params* P = &J->P;
+  const int d = P->d, nq = P->nq;
+  const size_t polyq = (size_t)nq * d;
+  memset(partial, 0, 8 * (size_t)(P->cols + 1) * polyq);
+  for (int i = 0; i <= P->cols; ++i)
+    for (int j = 0; j < P->rows; ++j)
+      for (int l = 0; l < nq; ++l)
+        mac_mont(partial + (size_t)i * polyq + (size_t)l * d, left + (size_t)j * polyq + (size_t)l * d,
+                 ob_enc + ((size_t)i * P->rows + j) * polyq + (size_t)l * d, &J->rq[l], d);
+}
+
+/* pf.Encode[i] = Enc[cols][i] + sum_j chals[j] * Enc[j][i]; pf.MLWE[i] likewise over the
+   inMSIS + mlwe MLWE polynomials (prover.go:300-314) */
+void of_jindo_eval_respond(const of_jindo* J, const uint64_t* ob_enc, const uint64_t* ob_mlwe, const uint64_t* chals,
+                           uint64_t* pf_enc, uint64_t* pf_mlwe) {
+  const of_jindo_params* P = &J->P;
+  const int d = P->d, nq = P->nq, nm = P->in_msis + P->mlwe;
+  const size_t polyq = (size_t)nq * d;
+  for (int i = 0; i < P->rows; ++i) {
+    memcpy(pf_enc + (size_t)i * polyq, ob_enc + ((size_t)P->cols * P->rows + i) * polyq, 8 * polyq);
+    for (int j = 0; j < P->cols; ++j)
+      for (int l = 0; l < nq; ++l)
+        mac_mont(pf_enc + (size_t)i * polyq + (size_t)l * d, chals + (size_t)j * polyq + (size_t)l * d,
+                 ob_enc + ((size_t)j * P->rows + i) * polyq + (size_t)l * d, &J->rq[l], d);
+  }
+  for (int i = 0; i < nm; ++i) {
+    memcpy(pf_mlwe + (size_t)i * polyq, ob_mlwe + ((size_t)P->cols * nm + i) * polyq, 8 * polyq);
+    for (int j = 0; j < P->cols; ++j)
+      for (int l = 0; l < nq; ++l)
+        mac_mont(pf_mlwe + (size_t)i * polyq + (size_t)l * d, chals + (size_t)j * polyq + (size_t)l * d,
+                 ob_mlwe + ((size_t)j * nm + i) * polyq + (size_t)l * d, &J->rq[l], d);
+  }
+}

@@ -1414,11 +1414,93 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   return RG_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Prover.Evaluate core (prover.go:205-324): the MulCoeffsMontgomeryThenAdd loops, with the
+// Fiat-Shamir challenges (batch, left, chals) injected by the caller.  Every loop is a
+// per-(limb, coeff) dot product, so each maps onto mac_kernel with J = 1 and the loop's own
+// strides.
+// ------------------------------------------------------------------------------------------
+static MacArgs dot_args(const RnsPrime* P, int nl, int d, long long nout, int T, const uint64_t* A, const uint64_t* B,
+                        long long b_out, long long b_term, uint64_t* out) {
+  MacArgs m;
+  memset(&m, 0, sizeof(m));
+  m.d = d;
+  m.nl = nl;
+  m.J = 1;
+  m.ncols = nout;
+  m.T1 = T;
+  m.A1 = A;
+  m.B1 = B;
+  m.b1_col = b_out;
+  m.b1_term = b_term;
+  m.out = out;
+  for (int l = 0; l < nl; ++l) m.P[l] = P[l];
+  return m;
+}
+
+static rg_status eval_batch(const rg_jindo* J, size_t batch, const uint64_t* incom, const uint64_t* enc,
+                            const uint64_t* mlwe, const uint64_t* bq, const uint64_t* bo, uint64_t* ob_incom,
+                            uint64_t* ob_enc, uint64_t* ob_mlwe, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  const long long pq = (long long)p.nq * p.d, po = (long long)p.nqo * p.d, nm = p.in_msis + p.mlwe;
+  const long long n_inc = p.dcmp, n_enc = (long long)(p.cols + 1) * p.rows, n_ml = (long long)(p.cols + 1) * nm;
+  if (batch == 1) {  // openBatch = open[0] (prover.go:267-269)
+    RG_HIP(hipMemcpyAsync(ob_incom, incom, 8 * n_inc * po, hipMemcpyDeviceToDevice, st));
+    RG_HIP(hipMemcpyAsync(ob_enc, enc, 8 * n_enc * pq, hipMemcpyDeviceToDevice, st));
+    RG_HIP(hipMemcpyAsync(ob_mlwe, mlwe, 8 * n_ml * pq, hipMemcpyDeviceToDevice, st));
+    return RG_OK;
+  }
+  const int T = (int)batch;  // term i = commit i, scaled by its batch challenge (:254-266)
+  RG_TRY(launch_mac(dot_args(J->ro, p.nqo, p.d, n_inc, T, bo, incom, po, n_inc * po, ob_incom), st));
+  RG_TRY(launch_mac(dot_args(J->rq, p.nq, p.d, n_enc, T, bq, enc, pq, n_enc * pq, ob_enc), st));
+  RG_TRY(launch_mac(dot_args(J->rq, p.nq, p.d, n_ml, T, bq, mlwe, pq, n_ml * pq, ob_mlwe), st));
+  return RG_OK;
+}
+
 }  // namespace rg
 
 using namespace rg;
 
 extern "C" {
+
+rg_status rg_jindo_eval_batch_dev(const rg_jindo* J, size_t batch, const uint64_t* d_incom, const uint64_t* d_enc,
+                                  const uint64_t* d_mlwe, const uint64_t* d_bq, const uint64_t* d_bo,
+                                  uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe, void* stream) {
+  if (!J || batch == 0 || !d_incom || !d_enc || !d_mlwe || !d_ob_incom || !d_ob_enc || !d_ob_mlwe ||
+      (batch > 1 && (!d_bq || !d_bo)))
+    return RG_ERR_INVALID;
+  return eval_batch(J, batch, d_incom, d_enc, d_mlwe, d_bq, d_bo, d_ob_incom, d_ob_enc, d_ob_mlwe, as_stream(stream));
+}
+
+rg_status rg_jindo_eval_partial_dev(const rg_jindo* J, const uint64_t* d_ob_enc, const uint64_t* d_left,
+                                    uint64_t* d_partial, void* stream) {
+  if (!J || !d_ob_enc || !d_left || !d_partial) return RG_ERR_INVALID;
+  const rg_jindo_params& p = J->p;
+  const long long pq = (long long)p.nq * p.d;
+  // out i in [0, cols]: sum_j left[j] * Enc[i][j] (prover.go:274-282); i = cols is PartialMask
+  return launch_mac(dot_args(J->rq, p.nq, p.d, p.cols + 1, p.rows, d_left, d_ob_enc, (long long)p.rows * pq, pq,
+                             d_partial),
+                    as_stream(stream));
+}
+
+rg_status rg_jindo_eval_respond_dev(const rg_jindo* J, const uint64_t* d_ob_enc, const uint64_t* d_ob_mlwe,
+                                    const uint64_t* d_chals, uint64_t* d_pf_enc, uint64_t* d_pf_mlwe, void* stream) {
+  if (!J || !d_ob_enc || !d_ob_mlwe || !d_chals || !d_pf_enc || !d_pf_mlwe) return RG_ERR_INVALID;
+  const rg_jindo_params& p = J->p;
+  const long long pq = (long long)p.nq * p.d, nm = p.in_msis + p.mlwe;
+  hipStream_t st = as_stream(stream);
+  // pf.Encode[i] = Enc[cols][i] + sum_j chals[j] * Enc[j][i] (prover.go:300-306)
+  MacArgs e = dot_args(J->rq, p.nq, p.d, p.rows, p.cols, d_chals, d_ob_enc, pq, (long long)p.rows * pq, d_pf_enc);
+  e.C = d_ob_enc + (long long)p.cols * p.rows * pq;
+  e.c_col = pq;
+  RG_TRY(launch_mac(e, st));
+  // pf.MLWE[i] = MLWE[cols][i] + sum_j chals[j] * MLWE[j][i] (:308-314)
+  MacArgs m = dot_args(J->rq, p.nq, p.d, nm, p.cols, d_chals, d_ob_mlwe, pq, nm * pq, d_pf_mlwe);
+  m.C = d_ob_mlwe + (long long)p.cols * nm * pq;
+  m.c_col = pq;
+  return launch_mac(m, st);
+}
+
 
 static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** J) {
   if (!out) return RG_ERR_INVALID;

@@ -156,5 +156,31 @@ class Prover:
                                         _stream(stream)))
 
 
+    # ---- Prover.Evaluate (jindo/prover.go:205-324), device-resident, challenges injected ----
+    # The Fiat-Shamir transcript, encodeChallengeTo, leftVec/encode and Poly.Evaluate stay with
+    # the caller (Go in the reference); these are its MulCoeffsMontgomeryThenAdd loops.
+    def eval_shapes(self):
+        P = self.params
+        nm = P.in_msis + P.mlwe
+        return dict(ob_incom=(P.dcmp, P.nqo, P.d), ob_enc=(P.cols + 1, P.rows, P.nq, P.d),
+                    ob_mlwe=(P.cols + 1, nm, P.nq, P.d), partial=(P.cols + 1, P.nq, P.d),
+                    pf_enc=(P.rows, P.nq, P.d), pf_mlwe=(nm, P.nq, P.d))
+
+    def eval_batch_dev(self, batch, incom, enc, mlwe, bq, bo, ob_incom, ob_enc, ob_mlwe, stream=None):
+        """openBatch = sum_i open[i] * batch[i] (prover.go:228-269); Proof.InCommit = ob_incom."""
+        check(lib().rg_jindo_eval_batch_dev(self.h, batch, _addr(incom), _addr(enc), _addr(mlwe), _addr(bq),
+                                            _addr(bo), _addr(ob_incom), _addr(ob_enc), _addr(ob_mlwe),
+                                            _stream(stream)))
+
+    def eval_partial_dev(self, ob_enc, left, partial, stream=None):
+        """Proof.Partial[0..cols) and PartialMask (= partial[cols]) (prover.go:274-282)."""
+        check(lib().rg_jindo_eval_partial_dev(self.h, _addr(ob_enc), _addr(left), _addr(partial), _stream(stream)))
+
+    def eval_respond_dev(self, ob_enc, ob_mlwe, chals, pf_enc, pf_mlwe, stream=None):
+        """Proof.Encode and Proof.MLWE (prover.go:300-314)."""
+        check(lib().rg_jindo_eval_respond_dev(self.h, _addr(ob_enc), _addr(ob_mlwe), _addr(chals), _addr(pf_enc),
+                                              _addr(pf_mlwe), _stream(stream)))
+
+
 def NewProver(params, crs):
     return Prover(params, crs=crs)
