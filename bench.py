@@ -143,7 +143,7 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L)
 
 
-def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world):
+def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world, eval_steps=0):
     """Device-resident batched commits (rg_jindo_commit_dev) at a BASELINE Jindo config.
     The commit key is derived from the CRS on rank 0 and broadcast once over RCCL (xGMI)."""
     from ringo import jindo
@@ -202,10 +202,54 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world)
         dist.barrier()
     wall = time.perf_counter() - t0
     nm = params.in_msis + params.mlwe
-    bytes_per_commit = 8 * (nv * L + params.dcmp * params.nqo * params.d + (params.cols + 1) * params.rows *
-                            params.nq * params.d + (params.cols + 1) * nm * params.nq * params.d +
-                            params.out_msis * params.nq * params.d)
-    return dict(wall_s=wall, kernel_ms=ev.total_ms(), commits=batch * steps, bytes_per_commit=bytes_per_commit)
+    opening_words = (params.dcmp * params.nqo * params.d + (params.cols + 1) * params.rows * params.nq * params.d +
+                     (params.cols + 1) * nm * params.nq * params.d)
+    bytes_per_commit = 8 * (nv * L + opening_words + params.out_msis * params.nq * params.d)
+    res = dict(wall_s=wall, kernel_ms=ev.total_ms(), commits=batch * steps, bytes_per_commit=bytes_per_commit)
+    if eval_steps and P["batch"] > 1:
+        res["eval"] = eval_bench(torch, prv, dist, P, params, batch, outs, eval_steps, g, dev, opening_words)
+    return res
+
+
+def eval_bench(torch, prv, dist, P, params, batch, outs, steps, g, dev, opening_words):
+    """Prover.Evaluate's device work (prover.go:228-314) over this GPU's shard of the batch
+    (`batch` openings just committed): batch combination, the cross-GPU all-reduce of the partial
+    openBatches (RCCL; none at N = 1) and mod-q fold, partial evaluations, responses.  The
+    challenges are injected device-generated residues (the SHAKE transcript stays host-side)."""
+    from ringo.shard import allreduce_open_batch
+    es = prv.eval_shapes()
+    q, qo = params.q, params.qo
+
+    def res(primes, shape):
+        t = torch.empty(shape, dtype=torch.int64, device=dev)
+        for l, qq in enumerate(primes):
+            t[..., l, :] = torch.randint(0, qq, t[..., l, :].shape, dtype=torch.int64, device=dev, generator=g)
+        return t
+
+    bq, bo = res(q, (batch, len(q), params.d)), res(qo, (batch, len(qo), params.d))
+    left, chals = res(q, (params.rows, len(q), params.d)), res(q, (params.cols, len(q), params.d))
+    o = {k: torch.empty(es[k], dtype=torch.int64, device=dev) for k in es}
+    stream = torch.cuda.current_stream()
+
+    def step():
+        prv.eval_batch_dev(batch, outs["incom"], outs["enc"], outs["mlwe_out"], bq, bo, o["ob_incom"], o["ob_enc"],
+                           o["ob_mlwe"], stream)
+        allreduce_open_batch(prv, dist, o["ob_incom"], o["ob_enc"], o["ob_mlwe"], stream)
+        prv.eval_partial_dev(o["ob_enc"], left, o["partial"], stream)
+        prv.eval_respond_dev(o["ob_enc"], o["ob_mlwe"], chals, o["pf_enc"], o["pf_mlwe"], stream)
+
+    step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ms = (time.perf_counter() - t0) * 1000.0 / steps
+    return dict(ms=ms, openings_per_gpu=batch, bytes_read=8 * opening_words * batch)
 
 
 def traffic_per_ntt():
@@ -341,7 +385,8 @@ def main():
                                            "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N}}
     for cfg, jb, key in (("t14_b1", args.j14_batch, "j14"), ("t16_b4096", args.j16_batch, "j16")):
         if key in extra:
-            jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world)
+            jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world,
+                             eval_steps=max(2, args.steps // 2))
             jms = jr["wall_s"] * 1000.0 / max(2, args.steps // 2)
             if dist is not None:
                 t = torch.tensor([jms], dtype=torch.float64, device="cuda")
@@ -355,6 +400,18 @@ def main():
                         "achieved_GBs": jr["bytes_per_commit"] * jr["commits"] / (jr["kernel_ms"] / 1000.0) / 1e9,
                         "bytes_per_commit": jr["bytes_per_commit"],
                         "randomness": "injected (device-generated integers); host Gaussian sampling not timed"}
+            if "eval" in jr:
+                ems = jr["eval"]["ms"]
+                if dist is not None:
+                    t = torch.tensor([ems], dtype=torch.float64, device="cuda")
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    ems = float(t[0])
+                out["jindo_evaluate_2e16"] = {
+                    "value": world * jb / (ems / 1000.0), "unit": "openings/s",
+                    "config": "configs[4] shape: Prover.Evaluate device work over the batch (%d openings per GPU): "
+                              "batch combination + RCCL all-reduce of partial openBatches + partial evaluations + "
+                              "responses; challenges injected" % jb,
+                    "ms_per_evaluate": ems, "achieved_GBs": jr["eval"]["bytes_read"] / (ems / 1000.0) / 1e9}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(P63, 1, args.logn, args.cpu_seconds)
     if rank == 0:

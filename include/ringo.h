@@ -178,7 +178,10 @@ size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
  * encodeChallengeTo, leftVec/encode and Poly.Evaluate stay in the Go caller, which also keeps
  * the shape panics (:206-216).  Challenge polynomials are ringQ / ringQOut residues in the
  * NTT + Montgomery domain, as Go holds them; every product is MulCoeffsMontgomeryThenAdd.
- * 1. openBatch = sum_i open[i] * batch[i] (:228-266), or open[0] when batch == 1 (:267-269):
+ * 1. openBatch = sum_i open[i] * batch[i] (:228-266); with d_bq = d_bo = NULL (params.batch == 1,
+ *    batch must be 1) openBatch = open[0] (:267-269).  A GPU holding a shard of a batch passes its
+ *    openings and their challenges; the shards' openBatches sum across GPUs (RCCL all-reduce of
+ *    the words, exact while n_gpus * q < 2^64) and rg_jindo_eval_reduce_dev folds them mod q.
  *      d_incom [batch][dcmp][nqo][d], d_enc [batch][cols+1][rows][nq][d],
  *      d_mlwe [batch][cols+1][in_msis+mlwe][nq][d]  the openings (rg_jindo_commit_dev layout)
  *      d_bq [batch][nq][d], d_bo [batch][nqo][d]     batch[i] in ringQ and batchOut[i] in ringQOut
@@ -186,6 +189,9 @@ size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
 rg_status rg_jindo_eval_batch_dev(const rg_jindo* j, size_t batch, const uint64_t* d_incom, const uint64_t* d_enc,
                                   const uint64_t* d_mlwe, const uint64_t* d_bq, const uint64_t* d_bo,
                                   uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe, void* stream);
+/* words mod q, in place, over an openBatch (after a cross-GPU sum of partial openBatches) */
+rg_status rg_jindo_eval_reduce_dev(const rg_jindo* j, uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe,
+                                   void* stream);
 /* 2. Proof.Partial[i] = sum_j left[j] * openBatch.Encode[i][j] (:274-278) and
  *    Proof.PartialMask over column cols (:280-282):
  *      d_left [rows][nq][d] (encode(leftVec(x)[j]))   d_partial [cols+1][nq][d], last = PartialMask */

@@ -1444,7 +1444,7 @@ static rg_status eval_batch(const rg_jindo* J, size_t batch, const uint64_t* inc
   const rg_jindo_params& p = J->p;
   const long long pq = (long long)p.nq * p.d, po = (long long)p.nqo * p.d, nm = p.in_msis + p.mlwe;
   const long long n_inc = p.dcmp, n_enc = (long long)(p.cols + 1) * p.rows, n_ml = (long long)(p.cols + 1) * nm;
-  if (batch == 1) {  // openBatch = open[0] (prover.go:267-269)
+  if (!bq) {  // params.batch == 1: openBatch = open[0] (prover.go:267-269)
     RG_HIP(hipMemcpyAsync(ob_incom, incom, 8 * n_inc * po, hipMemcpyDeviceToDevice, st));
     RG_HIP(hipMemcpyAsync(ob_enc, enc, 8 * n_enc * pq, hipMemcpyDeviceToDevice, st));
     RG_HIP(hipMemcpyAsync(ob_mlwe, mlwe, 8 * n_ml * pq, hipMemcpyDeviceToDevice, st));
@@ -1457,6 +1457,15 @@ static rg_status eval_batch(const rg_jindo* J, size_t batch, const uint64_t* inc
   return RG_OK;
 }
 
+// x mod q over limb-planar polynomials (Shoup by 1 reduces any 64-bit word): folds the
+// cross-GPU sum of partial openBatches (each < q, at most 2^64 / q of them) back to residues
+__global__ __launch_bounds__(256) void rns_reduce_kernel(uint64_t* x, long long npoly, int nl, int d, RingDev R) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npoly * nl * d) return;
+  const RnsPrime& P = R.p[(int)((i / d) % nl)];
+  x[i] = sh_mul(x[i], 1, P.one_sh, P.q);
+}
+
 }  // namespace rg
 
 using namespace rg;
@@ -1467,7 +1476,7 @@ rg_status rg_jindo_eval_batch_dev(const rg_jindo* J, size_t batch, const uint64_
                                   const uint64_t* d_mlwe, const uint64_t* d_bq, const uint64_t* d_bo,
                                   uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe, void* stream) {
   if (!J || batch == 0 || !d_incom || !d_enc || !d_mlwe || !d_ob_incom || !d_ob_enc || !d_ob_mlwe ||
-      (batch > 1 && (!d_bq || !d_bo)))
+      (!d_bq != !d_bo) || (!d_bq && batch != 1))
     return RG_ERR_INVALID;
   return eval_batch(J, batch, d_incom, d_enc, d_mlwe, d_bq, d_bo, d_ob_incom, d_ob_enc, d_ob_mlwe, as_stream(stream));
 }
@@ -1652,6 +1661,23 @@ rg_status rg_jindo_commit(const rg_jindo* J, const uint64_t* v, size_t nv, const
   RG_HIP(hipMemcpy(o_mlwe, ml_.p, b_ml, hipMemcpyDeviceToHost));
   RG_HIP(hipMemcpy(o_com, com_.p, b_com, hipMemcpyDeviceToHost));
   return RG_OK;
+}
+
+rg_status rg_jindo_eval_reduce_dev(const rg_jindo* J, uint64_t* d_ob_incom, uint64_t* d_ob_enc, uint64_t* d_ob_mlwe,
+                                   void* stream) {
+  if (!J || !d_ob_incom || !d_ob_enc || !d_ob_mlwe) return RG_ERR_INVALID;
+  const rg_jindo_params& p = J->p;
+  hipStream_t st = as_stream(stream);
+  const long long nm = p.in_msis + p.mlwe, n_enc = (long long)(p.cols + 1) * p.rows, n_ml = (long long)(p.cols + 1) * nm;
+  const RingDev rq = ring_dev(J->rq, p.nq, J->rootsq_f, J->rootsq_b), ro = ring_dev(J->ro, p.nqo, J->rootso_f, J->rootso_b);
+  auto go = [&](uint64_t* x, long long npoly, int nl, const RingDev& R) {
+    const long long n = npoly * nl * p.d;
+    hipLaunchKernelGGL(rns_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, npoly, nl, p.d, R);
+    return check_launch("jindo eval reduce");
+  };
+  RG_TRY(go(d_ob_incom, p.dcmp, p.nqo, ro));
+  RG_TRY(go(d_ob_enc, n_enc, p.nq, rq));
+  return go(d_ob_mlwe, n_ml, p.nq, rq);
 }
 
 }  // extern "C"

@@ -65,6 +65,7 @@ _SIGS = {
     "rg_jindo_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
     "rg_jindo_eval_batch_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "rg_jindo_eval_partial_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+    "rg_jindo_eval_reduce_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "rg_jindo_eval_respond_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
     "rg_malloc": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_size_t]),
     "rg_free": (ctypes.c_int, [vp]),

@@ -167,10 +167,15 @@ class Prover:
                     pf_enc=(P.rows, P.nq, P.d), pf_mlwe=(nm, P.nq, P.d))
 
     def eval_batch_dev(self, batch, incom, enc, mlwe, bq, bo, ob_incom, ob_enc, ob_mlwe, stream=None):
-        """openBatch = sum_i open[i] * batch[i] (prover.go:228-269); Proof.InCommit = ob_incom."""
+        """openBatch = sum_i open[i] * batch[i] (prover.go:228-269); Proof.InCommit = ob_incom.
+        bq = bo = None (params.batch == 1): openBatch = open[0]."""
         check(lib().rg_jindo_eval_batch_dev(self.h, batch, _addr(incom), _addr(enc), _addr(mlwe), _addr(bq),
                                             _addr(bo), _addr(ob_incom), _addr(ob_enc), _addr(ob_mlwe),
                                             _stream(stream)))
+
+    def eval_reduce_dev(self, ob_incom, ob_enc, ob_mlwe, stream=None):
+        """Words mod q in place (after summing partial openBatches across GPUs)."""
+        check(lib().rg_jindo_eval_reduce_dev(self.h, _addr(ob_incom), _addr(ob_enc), _addr(ob_mlwe), _stream(stream)))
 
     def eval_partial_dev(self, ob_enc, left, partial, stream=None):
         """Proof.Partial[0..cols) and PartialMask (= partial[cols]) (prover.go:274-282)."""

@@ -33,3 +33,23 @@ def broadcast_commit_key(ck, dist, device=None, src=0):
         res.append(out[off:off + n].reshape(a.shape))
         off += n
     return tuple(res)
+
+
+def allreduce_open_batch(prv, dist, ob_incom, ob_enc, ob_mlwe, stream=None):
+    """Sharded Prover.Evaluate batch combination (jindo/prover.go:254-266): every rank has run
+    rg_jindo_eval_batch_dev over its own commits (its slice of the batch challenges); the
+    partial openBatches (residues < q) are summed across ranks with ONE all-reduce over a flat
+    buffer (exact: world * q < 2^64 for the <= 60-bit ring primes) and folded mod q on device.
+    The tensors are int64 views of the uint64 words; they hold the full openBatch afterwards."""
+    import torch
+    if dist is None or dist.get_world_size() == 1:
+        return
+    P = prv.params
+    assert dist.get_world_size() * max(max(P.q), max(P.qo)) < 2 ** 64
+    flat = torch.cat([ob_incom.reshape(-1), ob_enc.reshape(-1), ob_mlwe.reshape(-1)])
+    dist.all_reduce(flat)  # int64 wrap-around addition == uint64 addition
+    n1, n2 = ob_incom.numel(), ob_enc.numel()
+    ob_incom.view(-1).copy_(flat[:n1])
+    ob_enc.view(-1).copy_(flat[n1:n1 + n2])
+    ob_mlwe.view(-1).copy_(flat[n1 + n2:])
+    prv.eval_reduce_dev(ob_incom, ob_enc, ob_mlwe, stream)

@@ -79,3 +79,68 @@ def test_two_rank_broadcast_and_shard():
     want = cf.ntt_fwd(allp, tw)
     got = np.concatenate([np.array(out[r][3], dtype=np.uint64) for r in range(world)])
     assert (got == want).all()
+
+
+def _eval_worker(rank, world, port, out):
+    """Sharded Evaluate batch combination: each rank combines its slice of the openings with the
+    C oracle (standing in for rg_jindo_eval_batch_dev), then ringo.shard.allreduce_open_batch
+    sums the partial openBatches over gloo; the mod-q fold (rg_jindo_eval_reduce_dev on the box)
+    is done on the CPU here."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "ringo-snark_amd"))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import coracle as co
+    from ringo.shard import allreduce_open_batch, shard_range
+    P = json.load(open(os.path.join(root, "tests", "golden", "jindo_params.json")))["t10_b8"]
+    cj = co.CJindo(P, int(P["field_q_hex"], 16))
+    es = cj.eval_shapes()
+    B = P["batch"]
+    rng = np.random.default_rng(21)
+
+    def res(primes, shape):
+        o = np.zeros(shape, np.uint64)
+        for l, qq in enumerate(primes):
+            o[..., l, :] = rng.integers(0, qq, size=o[..., l, :].shape, dtype=np.uint64)
+        return o
+
+    incom, enc = res(P["qo"], (B,) + es["ob_incom"]), res(P["q"], (B,) + es["ob_enc"])
+    mlwe = res(P["q"], (B,) + es["ob_mlwe"])
+    bq, bo = res(P["q"], (B, len(P["q"]), P["d"])), res(P["qo"], (B, len(P["qo"]), P["d"]))
+    lo, hi = shard_range(B, rank, world)
+    part = cj.eval_batch(incom[lo:hi], enc[lo:hi], mlwe[lo:hi], bq[lo:hi], bo[lo:hi])
+
+    class FakeProver:  # the parameters allreduce_open_batch reads, and a CPU mod-q fold
+        class params:
+            q, qo = P["q"], P["qo"]
+
+        @staticmethod
+        def eval_reduce_dev(a, b, c, stream=None):
+            for x, primes in ((a, P["qo"]), (b, P["q"]), (c, P["q"])):
+                v = x.numpy().view(np.uint64)
+                for l, qq in enumerate(primes):
+                    v[..., l, :] %= np.uint64(qq)
+
+    ts = [torch.from_numpy(part[k].view(np.int64).copy()) for k in ("ob_incom", "ob_enc", "ob_mlwe")]
+    allreduce_open_batch(FakeProver, dist, *ts)
+    whole = cj.eval_batch(incom, enc, mlwe, bq, bo)
+    out[rank] = all(bool((t.numpy().view(np.uint64) == whole[k]).all())
+                    for t, k in zip(ts, ("ob_incom", "ob_enc", "ob_mlwe")))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_evaluate_batch_allreduce():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_eval_worker, args=(world, port, out), nprocs=world, join=True)
+    assert out[0] and out[1]

@@ -166,8 +166,9 @@ def test_evaluate_core_matches_oracle(name):
     left = res(P["q"], (P["rows"], len(P["q"]), P["d"]))
     chals = res(P["q"], (P["cols"], len(P["q"]), P["d"]))
     out = {k: torch.zeros(es[k], dtype=torch.int64, device=dev) for k in es}
-    prv.eval_batch_dev(B, op["incom"], op["enc"], op["mlwe_out"], t(bq), t(bo), out["ob_incom"], out["ob_enc"],
-                       out["ob_mlwe"])
+    single = B == 1  # params.batch == 1: openBatch = open[0], no challenge (prover.go:267-269)
+    prv.eval_batch_dev(B, op["incom"], op["enc"], op["mlwe_out"], None if single else t(bq), None if single else t(bo),
+                       out["ob_incom"], out["ob_enc"], out["ob_mlwe"])
     prv.eval_partial_dev(out["ob_enc"], t(left), out["partial"])
     prv.eval_respond_dev(out["ob_enc"], out["ob_mlwe"], t(chals), out["pf_enc"], out["pf_mlwe"])
     torch.cuda.synchronize()
@@ -181,3 +182,43 @@ def test_evaluate_core_matches_oracle(name):
     pe, pm = cj.eval_respond(ob["ob_enc"], ob["ob_mlwe"], chals)
     assert (got["pf_enc"] == pe).all()
     assert (got["pf_mlwe"] == pm).all()
+
+
+def test_evaluate_batch_shards_sum_to_whole():
+    """A batch split across "ranks" (here: two shards on one GPU): each shard's partial openBatch,
+    summed word-wise (what the RCCL all-reduce does) and folded mod q by rg_jindo_eval_reduce_dev,
+    equals the single-GPU openBatch bit for bit."""
+    import torch
+    P, q, params = _setup("t10_b8")
+    prv = jindo.NewProver(params, b"Jindo!")
+    B = P["batch"]
+    dev = torch.device("cuda")
+    rng = np.random.default_rng(3)
+    es = prv.eval_shapes()
+
+    def res(primes, shape):
+        out = np.zeros(shape, np.uint64)
+        for l, qq in enumerate(primes):
+            out[..., l, :] = rng.integers(0, qq, size=out[..., l, :].shape, dtype=np.uint64)
+        return out
+
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    incom = t(res(P["qo"], (B,) + es["ob_incom"]))
+    enc = t(res(P["q"], (B,) + es["ob_enc"]))
+    mlwe = t(res(P["q"], (B,) + es["ob_mlwe"]))
+    bq, bo = t(res(P["q"], (B, len(P["q"]), P["d"]))), t(res(P["qo"], (B, len(P["qo"]), P["d"])))
+    zeros = lambda: {k: torch.zeros(es[k], dtype=torch.int64, device=dev) for k in ("ob_incom", "ob_enc", "ob_mlwe")}
+    whole = zeros()
+    prv.eval_batch_dev(B, incom, enc, mlwe, bq, bo, whole["ob_incom"], whole["ob_enc"], whole["ob_mlwe"])
+    parts = []
+    for lo, hi in ((0, 3), (3, B)):
+        o = zeros()
+        prv.eval_batch_dev(hi - lo, incom[lo:hi], enc[lo:hi], mlwe[lo:hi], bq[lo:hi], bo[lo:hi], o["ob_incom"],
+                           o["ob_enc"], o["ob_mlwe"])
+        parts.append(o)
+    summed = {k: parts[0][k] + parts[1][k] for k in parts[0]}
+    prv.eval_reduce_dev(summed["ob_incom"], summed["ob_enc"], summed["ob_mlwe"])
+    torch.cuda.synchronize()
+    for k in summed:
+        assert torch.equal(summed[k], whole[k]), k
+
