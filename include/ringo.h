@@ -110,6 +110,27 @@ rg_status rg_vec(const rg_field* f, int op, uint64_t* out, const uint64_t* a, co
 rg_status rg_vec_dev(const rg_field* f, int op, uint64_t* d_out, const uint64_t* d_a, const uint64_t* d_b, size_t n,
                      void* stream);
 
+/* ---- remaining bigpoly operators used by Buckler ------------- */
+/* CyclicEvaluator.QuoRemByVanishing(p, N) (math/bigpoly/cyclic.go:18-37): quotient and
+ * remainder of each of `batch` rank-coefficient polynomials by X^n_vanish - 1 (coefficient
+ * domain; the IsNTT / rank panics stay with the caller).  d_rem may alias d_p, d_quo may not. */
+rg_status rg_poly_quorem_vanishing_dev(const rg_field* f, size_t rank, long long n_vanish, uint64_t* d_quo,
+                                       uint64_t* d_rem, const uint64_t* d_p, size_t batch, void* stream);
+rg_status rg_poly_quorem_vanishing(const rg_field* f, size_t rank, long long n_vanish, uint64_t* quo, uint64_t* rem,
+                                   const uint64_t* p);
+/* CyclotomicEvaluator.AutTo(pOut, p, idx) (cyclotomic.go:29-86): X -> X^idx on each of `batch`
+ * polynomials, coefficient domain (ntt_domain = 0, autTo) or NTT domain (autNTTTo).  idx must
+ * be odd (RG_ERR_INVALID = the reference's "AutTo: idx must be odd" panic); d_out != d_p. */
+rg_status rg_poly_aut_dev(const rg_field* f, size_t rank, long long idx, int ntt_domain, uint64_t* d_out,
+                          const uint64_t* d_p, size_t batch, void* stream);
+rg_status rg_poly_aut(const rg_field* f, size_t rank, long long idx, int ntt_domain, uint64_t* out, const uint64_t* p);
+/* Poly.Evaluate(x) (poly.go:64-76): sum p_i x^i of n coefficients into ONE element d_out;
+ * d_scratch holds rg_poly_evaluate_scratch_bytes(f, n) bytes. */
+rg_status rg_poly_evaluate_dev(const rg_field* f, const uint64_t* d_p, size_t n, const uint64_t* d_x, uint64_t* d_out,
+                               uint64_t* d_scratch, void* stream);
+size_t rg_poly_evaluate_scratch_bytes(const rg_field* f, size_t n);
+rg_status rg_poly_evaluate(const rg_field* f, const uint64_t* p, size_t n, const uint64_t* x, uint64_t* out);
+
 /* ------------------------------------------------------------------------------------ */
 /* Jindo commitment (jindo/params.go, encoder.go, rns.go, prover.go, entities.go)         */
 /* ------------------------------------------------------------------------------------ */

@@ -32,6 +32,9 @@ def lib():
         L.of_ntt_fwd.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
         L.of_ntt_inv.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_long]
         L.of_vec.argtypes = [ctypes.c_void_p, ctypes.c_int, u64p, u64p, u64p, ctypes.c_long]
+        L.of_quorem_vanishing.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, u64p, u64p, u64p]
+        L.of_aut.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_int, u64p, u64p]
+        L.of_poly_evaluate.argtypes = [ctypes.c_void_p, u64p, ctypes.c_long, u64p, u64p]
         L.of_jindo_eval_batch.argtypes = [ctypes.c_void_p, ctypes.c_long] + [u64p] * 8
         L.of_jindo_eval_partial.argtypes = [ctypes.c_void_p, u64p, u64p, u64p]
         L.of_jindo_eval_respond.argtypes = [ctypes.c_void_p] + [u64p] * 5
@@ -96,6 +99,26 @@ class CField:
 
     def neg(self, x):
         return self._bin("of_f_neg", x)
+
+    # ---- bigpoly operators (cyclic.go:18-37, cyclotomic.go:29-86, poly.go:64-76) ----
+    def quorem_vanishing(self, p, N):
+        p = np.ascontiguousarray(p, np.uint64)
+        quo, rem = np.zeros_like(p), np.zeros_like(p)
+        lib().of_quorem_vanishing(self.buf, p.shape[0], N, ptr(quo), ptr(rem), ptr(p))
+        return quo, rem
+
+    def aut(self, p, idx, ntt):
+        p = np.ascontiguousarray(p, np.uint64)
+        out = np.zeros_like(p)
+        lib().of_aut(self.buf, p.shape[0], idx, 1 if ntt else 0, ptr(out), ptr(p))
+        return out
+
+    def evaluate(self, p, x):
+        p = np.ascontiguousarray(p, np.uint64)
+        xx = np.ascontiguousarray(x, np.uint64).reshape(self.L)
+        out = np.zeros(self.L, np.uint64)
+        lib().of_poly_evaluate(self.buf, ptr(p), p.shape[0], ptr(xx), ptr(out))
+        return out
 
     def tables(self, N, cyclic=False):
         """(tw [N,L], twinv [N,L], ninv [L]) as np.uint64 (Montgomery), or raises."""

@@ -846,3 +846,54 @@ void of_jindo_eval_respond(const of_jindo* J, const uint64_t* ob_enc, const uint
                  ob_mlwe + ((size_t)j * nm + i) * polyq + (size_t)l * d, &J->rq[l], d);
   }
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Remaining bigpoly operators, literal restatements                   */
+/* ------------------------------------------------------------------------------------------ */
+/* CyclicEvaluator.QuoRemByVanishing (cyclic.go:18-37); N >= 0 */
+void of_quorem_vanishing(const of_field* F, long rank, long N, uint64_t* quo, uint64_t* rem, const uint64_t* p) {
+  const int L = F->L;
+  memset(quo, 0, 8 * (size_t)rank * L);
+  memcpy(rem, p, 8 * (size_t)rank * L);
+  for (long i = rank - 1; i >= N; --i) {
+    f_add(F, quo + (size_t)(i - N) * L, quo + (size_t)(i - N) * L, rem + (size_t)i * L, L);
+    f_add(F, rem + (size_t)(i - N) * L, rem + (size_t)(i - N) * L, rem + (size_t)i * L, L);
+    memset(rem + (size_t)i * L, 0, 8 * (size_t)L);
+  }
+}
+/* CyclotomicEvaluator.AutTo (cyclotomic.go:29-86); idx odd */
+void of_aut(const of_field* F, long rank, long idx, int ntt, uint64_t* out, const uint64_t* p) {
+  const int L = F->L;
+  const long n2 = 2 * rank;
+  idx %= n2;
+  if (idx < 0) idx += n2;
+  uint64_t* buf = (uint64_t*)malloc(8 * (size_t)rank * L);
+  if (!ntt) { /* autTo (:53-67) */
+    for (long i = 0; i < rank; ++i) {
+      long j = (long)(((unsigned long)i * (unsigned long)idx) % (unsigned long)n2);
+      if (j < rank) memcpy(buf + (size_t)j * L, p + (size_t)i * L, 8 * (size_t)L);
+      else f_neg(F, buf + (size_t)(j - rank) * L, p + (size_t)i * L, L);
+    }
+    memcpy(out, buf, 8 * (size_t)rank * L);
+  } else { /* autNTTTo (:70-86) */
+    memcpy(buf, p, 8 * (size_t)rank * L);
+    bitrev_perm(buf, (int)rank, L);
+    for (long i = 0; i < rank; ++i) {
+      long j = (long)(((unsigned long)(2 * i + 1) * (unsigned long)idx) % (unsigned long)n2);
+      j = (j - 1) >> 1;
+      memcpy(out + (size_t)i * L, buf + (size_t)j * L, 8 * (size_t)L);
+    }
+    bitrev_perm(out, (int)rank, L);
+  }
+  free(buf);
+}
+/* Poly.Evaluate (poly.go:64-76): Horner from the top */
+void of_poly_evaluate(const of_field* F, const uint64_t* p, long n, const uint64_t* x, uint64_t* out) {
+  const int L = F->L;
+  uint64_t z[MAXL] = {0};
+  for (long i = n - 1; i >= 0; --i) {
+    f_mul(F, z, z, x, L);
+    f_add(F, z, z, p + (size_t)i * L, L);
+  }
+  memcpy(out, z, 8 * (size_t)L);
+}

@@ -54,6 +54,15 @@ _SIGS = {
     "rg_ntt_inv_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
     "rg_vec": (ctypes.c_int, [vp, ctypes.c_int, u64p, u64p, u64p, ctypes.c_size_t]),
     "rg_vec_dev": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, ctypes.c_size_t, vp]),
+    "rg_poly_quorem_vanishing_dev": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, vp, vp, vp,
+                                                    ctypes.c_size_t, vp]),
+    "rg_poly_quorem_vanishing": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, u64p, u64p, u64p]),
+    "rg_poly_aut_dev": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_int, vp, vp, ctypes.c_size_t,
+                                       vp]),
+    "rg_poly_aut": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_int, u64p, u64p]),
+    "rg_poly_evaluate_dev": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, vp, vp]),
+    "rg_poly_evaluate_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
+    "rg_poly_evaluate": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u64p, u64p]),
     "rg_jindo_create": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), u64p, u64p, u64p, ctypes.POINTER(vp)]),
     "rg_jindo_create_from_crs": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.POINTER(vp)]),

@@ -192,6 +192,15 @@ class Poly:
     def Clear(self):
         self.Coeffs[...] = 0
 
+    def Evaluate(self, x):  # poly.go:64-76
+        """p(x) for x one element ([L] Montgomery limbs); rg_poly_evaluate."""
+        if self.IsNTT:
+            raise RingoPanic("Evaluate: p is in NTT form")
+        out = np.zeros(self.field.L, np.uint64)
+        xx = np.ascontiguousarray(x, np.uint64).reshape(self.field.L)
+        check(lib().rg_poly_evaluate(self.field.h, ptr(self.Coeffs), self.Rank(), ptr(xx), ptr(out)))
+        return out
+
 
 _OPS = {"add": 0, "sub": 1, "neg": 2, "mul": 3, "smul": 4, "mul_add": 5, "mul_sub": 6, "smul_add": 7, "smul_sub": 8}
 
@@ -330,9 +339,34 @@ class _BaseOperator:
 class CyclotomicEvaluator(_BaseOperator):
     """NewCyclotomicEvaluator (cyclotomic.go:15-20)."""
 
+    def Aut(self, p, idx):  # cyclotomic.go:22-27
+        o = self.NewPoly(p.IsNTT)
+        self.AutTo(o, p, idx)
+        return o
+
+    def AutTo(self, pOut, p, idx):  # cyclotomic.go:29-47 (autTo / autNTTTo)
+        self._unary(pOut, p)
+        if idx % 2 == 0:
+            raise RingoPanic("AutTo: idx must be odd")
+        src = p.Coeffs.copy() if pOut is p else p.Coeffs  # the reference works through a pooled buffer
+        check(lib().rg_poly_aut(self.field.h, self.rank, int(idx), 1 if p.IsNTT else 0, ptr(pOut.Coeffs), ptr(src)))
+        pOut.IsNTT = p.IsNTT
+
 
 class CyclicEvaluator(_BaseOperator):
     """NewCyclicEvaluator (cyclic.go:11-16)."""
+
+    def QuoRemByVanishing(self, p, N):  # cyclic.go:18-37
+        if p.Rank() != self.rank:
+            raise RingoPanic("inputs not consistent")
+        if p.IsNTT:
+            raise RingoPanic("input in NTT domain")
+        if N < 0:
+            raise RingoPanic("index out of range")  # Go: quo.Coeffs[i-N] with N < 0
+        quo, rem = self.NewPoly(False), self.NewPoly(False)
+        check(lib().rg_poly_quorem_vanishing(self.field.h, self.rank, int(N), ptr(quo.Coeffs), ptr(rem.Coeffs),
+                                             ptr(p.Coeffs)))
+        return quo, rem
 
 
 def NewCyclotomicEvaluator(field, rank):
