@@ -287,6 +287,44 @@ def vec_mul_bench(torch, ringo, q, L, n, steps, seed):
     return dict(elems_per_s=n / (ms * 1e-3), achieved_GBs=3 * 8 * L * n / (ms * 1e-3) / 1e9, ms=ms)
 
 
+def polyops_bench(torch, ringo, q, L, rank, batch, steps, seed):
+    """The remaining bigpoly operators at the configs[3] shape (q255, N = 2^16), device-resident:
+    AutTo in the NTT domain (cyclotomic.go:70-86) and QuoRemByVanishing by X^(N/2) - 1
+    (cyclic.go:18-37) over `batch` polynomials, Poly.Evaluate (poly.go:64-76) of one.  Bytes:
+    one read + one write (Aut), one read + two writes (QuoRem) of 8L B per coefficient."""
+    from ringo._lib import check, lib
+    dev = torch.device("cuda", torch.cuda.current_device())
+    F = ringo.Field(q)
+    x = torch.from_numpy(uniform_elems(q, L, batch * rank, seed).view(np.int64).reshape(-1)).to(dev)
+    o1, o2 = torch.empty_like(x), torch.empty_like(x)
+    xe = x[:L].clone()
+    ev_out = torch.empty(L, dtype=torch.int64, device=dev)
+    scratch = torch.empty(max(1, lib().rg_poly_evaluate_scratch_bytes(F.h, rank) // 8), dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream()
+    sp = st.cuda_stream
+    res = {}
+    for name, fn, nbytes in (
+            ("aut_ntt", lambda: check(lib().rg_poly_aut_dev(F.h, rank, 5, 1, o1.data_ptr(), x.data_ptr(), batch, sp)),
+             2 * 8 * L * rank * batch),
+            ("quorem_vanishing", lambda: check(lib().rg_poly_quorem_vanishing_dev(
+                F.h, rank, rank // 2, o1.data_ptr(), o2.data_ptr(), x.data_ptr(), batch, sp)), 3 * 8 * L * rank * batch),
+            ("evaluate", lambda: check(lib().rg_poly_evaluate_dev(F.h, x.data_ptr(), rank, xe.data_ptr(),
+                                                                  ev_out.data_ptr(), scratch.data_ptr(), sp)),
+             8 * L * rank)):
+        fn()
+        torch.cuda.synchronize()
+        ev = Events(torch, st)
+        ev.start()
+        for _ in range(steps):
+            fn()
+        ev.stop()
+        torch.cuda.synchronize()
+        ms = ev.total_ms() / steps
+        res[name] = {"ms": ms, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9}
+    res["shape"] = "N=2^16, q255 (L=4); aut/quorem over %d polys, evaluate of one" % batch
+    return res
+
+
 def cpu_baseline(q, L, logn, seconds):
     """C restatement (oracle/liboracle.so) fwd+inv on this host: bounded sample, all threads
     the OpenMP runtime gives it (OMP_NUM_THREADS)."""
@@ -382,7 +420,8 @@ def main():
                          "achieved_GBs": 2 * N * 32 * r4["ntts"] / (r4["kernel_ms"] / 1000.0) / 1e9,
                          "selfcheck_fwd_inv_identity": r4["ok"],
                          "pointwise_mul": {"unit": "elements/s", "value": world * vm["elems_per_s"],
-                                           "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N}}
+                                           "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N},
+                         "bigpoly_ops": polyops_bench(torch, ringo, Q255, 4, N, 64, 10, 13 + rank)}
     for cfg, jb, key in (("t14_b1", args.j14_batch, "j14"), ("t16_b4096", args.j16_batch, "j16")):
         if key in extra:
             jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world,

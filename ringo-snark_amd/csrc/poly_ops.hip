@@ -6,8 +6,9 @@
 //   * CyclotomicEvaluator.AutTo (cyclotomic.go:29-86): coefficient domain as a signed scatter
 //     (j = i idx mod 2N, negated when j >= N), NTT domain as one gather through the bit
 //     reversals (out[k] = p[brv(((2 brv(k) + 1) idx mod 2N - 1) / 2)]);
-//   * Poly.Evaluate (poly.go:64-76): Horner per 64-coefficient chunk (one lane each), then the
-//     chunk values combined by a single-workgroup Horner in x^64 -- the same field element.
+//   * Poly.Evaluate (poly.go:64-76): a Horner tree -- Horner over 64-coefficient chunks (one
+//     lane each) in x, then over 64-value chunks of those in x^64, ... down to one value; the
+//     same field element as the reference's single Horner pass.
 // All field arithmetic is the Montgomery form of field.hpp (gnark's representation), so every
 // output limb equals the reference's.
 #include <cstring>
@@ -113,37 +114,33 @@ __global__ __launch_bounds__(256) void aut_ntt_kernel(PolyArgs<L> a) {
 // ---- Evaluate -------------------------------------------------------------------------------
 constexpr int kEvalChunk = 64;
 
-// chunk c: sum_{i < 64} p[64 c + i] x^i by Horner (z = z x + p_i from the top, poly.go:71-74)
+// one level of a Horner tree: out[c] = sum_{i < 64} in[64 c + i] y^i (z = z y + in_i from the
+// top, poly.go:71-74), y = x^(64^level); the level-0 input is the polynomial itself
 template <int L>
-__global__ __launch_bounds__(256) void eval_chunk_kernel(PolyArgs<L> a, const uint64_t* x) {
+__global__ __launch_bounds__(256) void eval_level_kernel(FieldParams<L> F, const uint64_t* in, long long n,
+                                                         const uint64_t* y, uint64_t* out) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.m) return;
-  uint64_t xv[L], z[L] = {0};
-  cp<L>(xv, x);
-  const long long lo = c * kEvalChunk, hi = min(a.rank, lo + kEvalChunk);
+  if (c >= (n + kEvalChunk - 1) / kEvalChunk) return;
+  uint64_t yv[L], z[L] = {0};
+  cp<L>(yv, y);
+  const long long lo = c * kEvalChunk, hi = min(n, lo + kEvalChunk);
   for (long long i = hi - 1; i >= lo; --i) {
     uint64_t t[L], pi[L];
-    f_mul<L>(t, z, xv, a.F);
-    cp<L>(pi, a.in + i * L);
-    f_add<L>(z, t, pi, a.F);
+    f_mul<L>(t, z, yv, F);
+    cp<L>(pi, in + i * L);
+    f_add<L>(z, t, pi, F);
   }
-  cp<L>(a.out + c * L, z);
+  cp<L>(out + c * L, z);
 }
 
-// one lane: y = x^64 by squaring, then Horner over the chunk values in y
+// y' = y^64 (six squarings), one lane
 template <int L>
-__global__ void eval_combine_kernel(PolyArgs<L> a, const uint64_t* x, uint64_t* result) {
+__global__ void eval_pow_kernel(FieldParams<L> F, const uint64_t* y, uint64_t* out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t y[L], z[L] = {0};
-  cp<L>(y, x);
-  for (int s = 0; s < 6; ++s) f_mul<L>(y, y, y, a.F);  // x^(2^6) = x^kEvalChunk
-  for (long long c = a.m - 1; c >= 0; --c) {
-    uint64_t t[L], v[L];
-    f_mul<L>(t, z, y, a.F);
-    cp<L>(v, a.out + c * L);
-    f_add<L>(z, t, v, a.F);
-  }
-  cp<L>(result, z);
+  uint64_t v[L];
+  cp<L>(v, y);
+  for (int s = 0; s < 6; ++s) f_mul<L>(v, v, v, F);
+  cp<L>(out, v);
 }
 
 template <int L>
@@ -191,18 +188,31 @@ static rg_status aut_L(const rg_field* f, long long rank, long long idx, bool nt
   return check_launch("aut");
 }
 
+// levels: n -> ceil(n/64) -> ... -> 1 value; scratch holds two value arrays and two powers
 template <int L>
 static rg_status eval_L(const rg_field* f, const uint64_t* p, long long n, const uint64_t* x, uint64_t* out,
                         uint64_t* scratch, hipStream_t st) {
-  PolyArgs<L> a = args_of<L>(f);
-  a.in = p;
-  a.rank = n;
-  a.m = (n + kEvalChunk - 1) / kEvalChunk;
-  a.out = scratch;
-  hipLaunchKernelGGL(eval_chunk_kernel<L>, dim3(grid_of(a.m)), dim3(256), 0, st, a, x);
-  RG_TRY(check_launch("evaluate chunks"));
-  hipLaunchKernelGGL(eval_combine_kernel<L>, dim3(1), dim3(64), 0, st, a, x, out);
-  return check_launch("evaluate combine");
+  const PolyArgs<L> a = args_of<L>(f);
+  const long long m0 = (n + kEvalChunk - 1) / kEvalChunk;
+  uint64_t* buf[2] = {scratch, scratch + m0 * L};
+  uint64_t* pw[2] = {scratch + 2 * m0 * L, scratch + 2 * m0 * L + L};
+  const uint64_t* src = p;
+  const uint64_t* y = x;
+  long long cur = n;
+  int lvl = 0;
+  for (;;) {
+    const long long m = (cur + kEvalChunk - 1) / kEvalChunk;
+    uint64_t* dst = m == 1 ? out : buf[lvl & 1];
+    hipLaunchKernelGGL(eval_level_kernel<L>, dim3(grid_of(m)), dim3(256), 0, st, a.F, src, cur, y, dst);
+    RG_TRY(check_launch("evaluate level"));
+    if (m == 1) return RG_OK;
+    hipLaunchKernelGGL(eval_pow_kernel<L>, dim3(1), dim3(64), 0, st, a.F, y, pw[lvl & 1]);
+    RG_TRY(check_launch("evaluate power"));
+    y = pw[lvl & 1];
+    src = dst;
+    cur = m;
+    ++lvl;
+  }
 }
 
 #define RG_DISPATCH_L(L_, CALL)                 \
@@ -268,7 +278,7 @@ rg_status rg_poly_evaluate_dev(const rg_field* f, const uint64_t* d_p, size_t n,
 }
 
 size_t rg_poly_evaluate_scratch_bytes(const rg_field* f, size_t n) {
-  return f ? ((n + kEvalChunk - 1) / kEvalChunk) * f->L * 8 : 0;
+  return f ? (2 * ((n + kEvalChunk - 1) / kEvalChunk) + 2) * f->L * 8 : 0;
 }
 
 // host-pointer forms (cgo drop-in; stage through device buffers)
