@@ -663,54 +663,61 @@ __device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
   a.s00 = a.s01 = a.s11 = 0;
 }
 
-template <int JP>
-__global__ __launch_bounds__(512) void mac3_kernel(Mac3Args a) {
-  static_assert(JP * 8 * 64 <= 2 * kMac3Tc * 8 * 64, "output stage must fit the tile buffers");
-  __shared__ uint64_t lds[2 * kMac3Tc * 8 * 64];  // two B tiles [tt][lk8][col]; then the output stage
-  __shared__ uint64_t lda[2][8][kMac3Tc * JP];     // two key tiles [w][tt][j]
+// JS = 2 splits the JP outputs of a (column, lk) across two waves (JP / 2 accumulators each):
+// a workgroup then covers 64 columns x 4 lk, the register file holds half as many accumulators
+// per lane (<= 128 VGPRs), and two workgroups (16 waves) share a CU instead of one.
+template <int JP, int JS>
+__global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) {
+  constexpr int NLK = 8 / JS, JW = JP / JS;  // lk per workgroup, accumulators per lane
+  static_assert(JP * NLK * 64 <= 2 * kMac3Tc * NLK * 64, "output stage must fit the tile buffers");
+  static_assert(JW % 2 == 0 && NLK % 2 == 0, "16-B staging");
+  __shared__ uint64_t lds[2 * kMac3Tc * NLK * 64];  // two B tiles [tt][lk][col]; then the output stage
+  __shared__ uint64_t lda[2][NLK][kMac3Tc * JP];    // two key tiles [lk][tt][j]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long long nlkg = a.per_col / 8;
-  const long long lk0 = (blockIdx.x % nlkg) * 8, c0 = (blockIdx.x / nlkg) * 64;
-  const int lk = (int)lk0 + w;
+  const int lkw = w % NLK, jh = w / NLK;  // this wave's lk and output half
+  const long long nlkg = a.per_col / NLK;
+  const long long lk0 = (blockIdx.x % nlkg) * NLK, c0 = (blockIdx.x / nlkg) * 64;
+  const int lk = (int)lk0 + lkw;
   const int T = a.T1 + a.T2;
-  // loader role: column c0 + lane, term tb + w, 8 consecutive lk (64 B)
+  // loader role: column c0 + lane, term tb + w, NLK consecutive lk (8 NLK bytes)
   const long long lcol = c0 + lane;
   const bool lval = lcol < a.ncols;
-  auto gload = [&](int tb, ulonglong2 (&v)[4]) {
+  auto gload = [&](int tb, ulonglong2 (&v)[NLK / 2]) {
     const int t = tb + w;
     if (lval && t < T) {
       const uint64_t* p = t < a.T1 ? a.B1 + lcol * a.b1_col + (long long)t * a.b1_term + lk0
                                    : a.B2 + lcol * a.b2_col + (long long)(t - a.T1) * a.b2_term + lk0;
       const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = q[i];
+      for (int i = 0; i < NLK / 2; ++i) v[i] = q[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = make_ulonglong2(0, 0);
+      for (int i = 0; i < NLK / 2; ++i) v[i] = make_ulonglong2(0, 0);
     }
   };
-  auto lstore = [&](int buf, const ulonglong2 (&v)[4]) {
-    uint64_t* L = lds + buf * (kMac3Tc * 8 * 64) + (w * 8) * 64 + lane;
+  auto lstore = [&](int buf, const ulonglong2 (&v)[NLK / 2]) {
+    uint64_t* L = lds + buf * (kMac3Tc * NLK * 64) + (w * NLK) * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NLK / 2; ++i) {
       L[(2 * i) * 64] = v[i].x;
       L[(2 * i + 1) * 64] = v[i].y;
     }
   };
-  // key loader role: lane < 4 JP loads 16 B of wave w's slice (8 terms x JP words)
+  // key loader role: wave (lkw, jh) stages its own half of lk's slice (8 terms x JW words)
   const ulonglong2* Aw = reinterpret_cast<const ulonglong2*>(a.As + (long long)lk * T * JP);
   auto aload = [&](int tb, ulonglong2& v) {
-    const int tt = lane / (JP / 2);
-    v = (lane < 4 * JP && tb + tt < T) ? Aw[(long long)tb * (JP / 2) + lane] : make_ulonglong2(0, 0);
+    const int tt = lane / (JW / 2), jj = lane % (JW / 2);
+    v = (lane < 4 * JW && tb + tt < T) ? Aw[((long long)(tb + tt) * JP + jh * JW) / 2 + jj] : make_ulonglong2(0, 0);
   };
   auto astore = [&](int buf, const ulonglong2& v) {
-    if (lane < 4 * JP) reinterpret_cast<ulonglong2*>(lda[buf][w])[lane] = v;
+    const int tt = lane / (JW / 2), jj = lane % (JW / 2);
+    if (lane < 4 * JW) reinterpret_cast<ulonglong2*>(lda[buf][lkw])[(tt * JP + jh * JW) / 2 + jj] = v;
   };
-  Mac3Acc acc[JP];
+  Mac3Acc acc[JW];
 #pragma unroll
-  for (int j = 0; j < JP; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
-  ulonglong2 pre[4], apre;
+  for (int j = 0; j < JW; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
+  ulonglong2 pre[NLK / 2], apre;
   gload(0, pre);
   aload(0, apre);
   lstore(0, pre);
@@ -723,16 +730,15 @@ __global__ __launch_bounds__(512) void mac3_kernel(Mac3Args a) {
       gload(tb + kMac3Tc, pre);
       aload(tb + kMac3Tc, apre);
     }
-    const uint64_t* L = lds + buf * (kMac3Tc * 8 * 64) + w * 64 + lane;
-    const uint64_t* LA = lda[buf][w];
+    const uint64_t* L = lds + buf * (kMac3Tc * NLK * 64) + lkw * 64 + lane;
+    const uint64_t* LA = lda[buf][lkw] + jh * JW;
 #pragma unroll
     for (int tt = 0; tt < kMac3Tc; ++tt) {
-      const int t = tb + tt;
-      if (t >= T) break;
-      const uint64_t b = L[tt * 8 * 64];
+      // terms past T were staged as zeros (B and key), so they add nothing
+      const uint64_t b = L[tt * NLK * 64];
       const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29);
 #pragma unroll
-      for (int j = 0; j < JP; ++j) {
+      for (int j = 0; j < JW; ++j) {
         const uint64_t av = LA[tt * JP + j];
         const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32);
         Mac3Acc& z = acc[j];
@@ -745,7 +751,7 @@ __global__ __launch_bounds__(512) void mac3_kernel(Mac3Args a) {
     since += kMac3Tc;
     if (since >= a.fold) {
 #pragma unroll
-      for (int j = 0; j < JP; ++j) mac3_fold(acc[j]);
+      for (int j = 0; j < JW; ++j) mac3_fold(acc[j]);
       since = 0;
     }
     if (more) {
@@ -759,34 +765,34 @@ __global__ __launch_bounds__(512) void mac3_kernel(Mac3Args a) {
   const RnsPrime& P = a.P[lk / a.d];
   const uint64_t q = P.q;
 #pragma unroll
-  for (int j = 0; j < JP; ++j) {
+  for (int j = 0; j < JW; ++j) {
     mac3_fold(acc[j]);
     uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
     r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
-    lds[(j * 8 + w) * 64 + lane] = r;  // [j][lk8][col]
+    lds[((jh * JW + j) * NLK + lkw) * 64 + lane] = r;  // [j][lk][col]
   }
   __syncthreads();
-  // store: (col, j) pairs, 8 consecutive lk = one 64-B row each
+  // store: (col, j) pairs, NLK consecutive lk = one 8 NLK-byte row each
+  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // NLK lk never straddle a limb (d % 8 == 0)
   for (int pidx = tid; pidx < JP * 64; pidx += 512) {
     const int c = pidx & 63, j = pidx >> 6;
     const long long col = c0 + c;
     if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r[8];
+    uint64_t r[NLK];
 #pragma unroll
-    for (int x = 0; x < 8; ++x) r[x] = lds[(j * 8 + x) * 64 + c];
+    for (int x = 0; x < NLK; ++x) r[x] = lds[(j * NLK + x) * 64 + c];
     if (a.C) {
       const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NLK / 2; ++i) {
         const ulonglong2 cv = cp[i];
-        const uint64_t qa = a.P[(int)((lk0 + 2 * i) / a.d)].q;  // 8 lk never straddle a limb (d % 8 == 0)
         r[2 * i] = mod_add(cv.x, r[2 * i], qa);
         r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
       }
     }
     ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
+    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
   }
 }
 
@@ -820,15 +826,27 @@ static bool mac3_ok(const RnsPrime* P, int nl, int J, int T, int d) {
 }
 
 static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
-  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
+  // RINGO_JINDO_MAC3_SPLIT=2 splits JP = 16 across two waves (measured slower: 19.4 vs 17.7 ms
+  // per configs[4] batch -- twice the LDS reads of each data word, 3 VGPRs spilled)
+  static const int split = [] {
+    const char* e = getenv("RINGO_JINDO_MAC3_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  const int jp = mac3_jp(m.J), js = (jp == 16 && split == 2) ? 2 : 1;
+  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / (8 / js));
   const dim3 g((unsigned)blocks), b(512);
-  switch (mac3_jp(m.J)) {
-    case 4: hipLaunchKernelGGL(mac3_kernel<4>, g, b, 0, st, m); break;
-    case 6: hipLaunchKernelGGL(mac3_kernel<6>, g, b, 0, st, m); break;
-    case 8: hipLaunchKernelGGL(mac3_kernel<8>, g, b, 0, st, m); break;
-    case 10: hipLaunchKernelGGL(mac3_kernel<10>, g, b, 0, st, m); break;
-    case 12: hipLaunchKernelGGL(mac3_kernel<12>, g, b, 0, st, m); break;
-    default: hipLaunchKernelGGL(mac3_kernel<16>, g, b, 0, st, m); break;
+  switch (jp) {
+    case 4: hipLaunchKernelGGL((mac3_kernel<4, 1>), g, b, 0, st, m); break;
+    case 6: hipLaunchKernelGGL((mac3_kernel<6, 1>), g, b, 0, st, m); break;
+    case 8: hipLaunchKernelGGL((mac3_kernel<8, 1>), g, b, 0, st, m); break;
+    case 10: hipLaunchKernelGGL((mac3_kernel<10, 1>), g, b, 0, st, m); break;
+    case 12: hipLaunchKernelGGL((mac3_kernel<12, 1>), g, b, 0, st, m); break;
+    default:
+      if (js == 2)
+        hipLaunchKernelGGL((mac3_kernel<16, 2>), g, b, 0, st, m);
+      else
+        hipLaunchKernelGGL((mac3_kernel<16, 1>), g, b, 0, st, m);
+      break;
   }
   return check_launch("jindo mac3");
 }
