@@ -663,9 +663,9 @@ __device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
   a.s00 = a.s01 = a.s11 = 0;
 }
 
-// JS = 2 splits the JP outputs of a (column, lk) across two waves (JP / 2 accumulators each):
-// a workgroup then covers 64 columns x 4 lk, the register file holds half as many accumulators
-// per lane (<= 128 VGPRs), and two workgroups (16 waves) share a CU instead of one.
+// JS = 2 would split the JP outputs of a (column, lk) across two waves (JP / 2 accumulators each,
+// 64 columns x 4 lk per workgroup, two workgroups per CU); measured slower at J = 10 and 16
+// (DESIGN.md §5), so only JS = 1 is instantiated.
 template <int JP, int JS>
 __global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) {
   constexpr int NLK = 8 / JS, JW = JP / JS;  // lk per workgroup, accumulators per lane
@@ -826,14 +826,8 @@ static bool mac3_ok(const RnsPrime* P, int nl, int J, int T, int d) {
 }
 
 static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
-  // RINGO_JINDO_MAC3_SPLIT=2 splits JP = 16 across two waves (measured slower: 19.4 vs 17.7 ms
-  // per configs[4] batch -- twice the LDS reads of each data word, 3 VGPRs spilled)
-  static const int split = [] {
-    const char* e = getenv("RINGO_JINDO_MAC3_SPLIT");
-    return e ? atoi(e) : 1;
-  }();
-  const int jp = mac3_jp(m.J), js = (jp == 16 && split == 2) ? 2 : 1;
-  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / (8 / js));
+  const int jp = mac3_jp(m.J);
+  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
   const dim3 g((unsigned)blocks), b(512);
   switch (jp) {
     case 4: hipLaunchKernelGGL((mac3_kernel<4, 1>), g, b, 0, st, m); break;
@@ -841,12 +835,7 @@ static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
     case 8: hipLaunchKernelGGL((mac3_kernel<8, 1>), g, b, 0, st, m); break;
     case 10: hipLaunchKernelGGL((mac3_kernel<10, 1>), g, b, 0, st, m); break;
     case 12: hipLaunchKernelGGL((mac3_kernel<12, 1>), g, b, 0, st, m); break;
-    default:
-      if (js == 2)
-        hipLaunchKernelGGL((mac3_kernel<16, 2>), g, b, 0, st, m);
-      else
-        hipLaunchKernelGGL((mac3_kernel<16, 1>), g, b, 0, st, m);
-      break;
+    default: hipLaunchKernelGGL((mac3_kernel<16, 1>), g, b, 0, st, m); break;
   }
   return check_launch("jindo mac3");
 }
