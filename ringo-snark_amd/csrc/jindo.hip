@@ -882,14 +882,17 @@ __device__ __forceinline__ void mw_muladd(uint64_t* v, int nw, uint64_t m, uint6
 }
 
 __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
-  __shared__ uint64_t poly[kMaxQ][kMaxD];
+  // LDS sized per launch (max(ns, nd) limbs x d words), not for kMaxQ x kMaxD: occupancy is then
+  // register-limited (7 waves/SIMD) instead of LDS-limited (5)
+  extern __shared__ uint64_t poly_lds[];
   const int d = a.d, tid = threadIdx.x, ns = a.src.n, nd = a.dst.n;
+  auto poly = [&](int l) { return poly_lds + (long long)l * d; };
   const long long pid = blockIdx.x;
   const uint64_t* in = a.in + pid * ns * d;
   for (int k = tid; k < ns * d; k += blockDim.x) {
     const int l = k / d;
     const RnsPrime& P = a.src.p[l];
-    poly[l][k % d] = sh_mul(in[k], P.rinv, P.rinv_sh, P.q);  // IMForm
+    poly(l)[k % d] = sh_mul(in[k], P.rinv, P.rinv_sh, P.q);  // IMForm
   }
   __syncthreads();
   const int half = blockDim.x >> 1;
@@ -897,12 +900,12 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
     const int l = l0 + (tid >= half ? 1 : 0);
     const bool active = l < ns;
     const int lc = active ? l : l0;
-    intt_lds(poly[lc], d, a.src.bwd + (long long)lc * d, a.src.p[lc], tid % half, half, active);
+    intt_lds(poly(lc), d, a.src.bwd + (long long)lc * d, a.src.p[lc], tid % half, half, active);
   }
   // CRT per coefficient
   for (int k = tid; k < d; k += blockDim.x) {
     uint64_t r[kMaxQ];
-    for (int l = 0; l < ns; ++l) r[l] = poly[l][k];
+    for (int l = 0; l < ns; ++l) r[l] = poly(l)[k];
     bool neg;
     uint64_t mag[4] = {0, 0, 0, 0};
     if (ns == 1) {  // reconstructTo fast path: toBalanced (rns.go:68-73,78-91)
@@ -963,17 +966,17 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
       if (neg && !zero) m = mod_neg(m, q);
       r[l] = sh_mul(m, P.r64, P.r64_sh, q);
     }
-    for (int l = 0; l < nd; ++l) poly[l][k] = r[l];  // each thread owns coefficient k
+    for (int l = 0; l < nd; ++l) poly(l)[k] = r[l];  // each thread owns coefficient k
   }
   __syncthreads();
   for (int l0 = 0; l0 < nd; l0 += 2) {
     const int l = l0 + (tid >= half ? 1 : 0);
     const bool active = l < nd;
     const int lc = active ? l : l0;
-    ntt_lds(poly[lc], d, a.dst.fwd + (long long)lc * d, a.dst.p[lc].q, tid % half, half, active);
+    ntt_lds(poly(lc), d, a.dst.fwd + (long long)lc * d, a.dst.p[lc].q, tid % half, half, active);
   }
   uint64_t* out = a.out + pid * a.out_stride;
-  for (int k = tid; k < a.out_rows * d; k += blockDim.x) out[k] = (k / d < nd) ? poly[k / d][k % d] : 0;
+  for (int k = tid; k < a.out_rows * d; k += blockDim.x) out[k] = (k / d < nd) ? poly(k / d)[k % d] : 0;
 }
 
 }  // namespace rg
@@ -1386,7 +1389,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   ra.out_rows = nqo;
   {
     const long long npoly = (long long)batch * (p.cols + 1) * p.in_msis;  // == batch * dcmp, same order
-    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), 0, st, ra);
+    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
     RG_TRY(check_launch("jindo round(in)"));
   }
   // 5. outer MAC + round -> Commitment.Value (ringQ-shaped rows, rows >= nqo zero)
@@ -1416,7 +1419,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   ro.out = d_com;
   ro.out_stride = (long long)nq * d;
   ro.out_rows = nq;
-  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), 0, st, ro);
+  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), (size_t)nqo * d * 8, st, ro);
   RG_TRY(check_launch("jindo round(out)"));
   return RG_OK;
 }
