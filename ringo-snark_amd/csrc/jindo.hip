@@ -1,23 +1,28 @@
-// jindo.hip -- the Jindo commitment (jindo/prover.go:45-202) on gfx950, batched over
-// independent commits, with the prover's randomness injected (include/ringo.h).
+// jindo.hip -- the Jindo commitment (jindo/prover.go:45-202) and the device work of
+// Prover.Evaluate (prover.go:205-324) on gfx950, batched over independent commits, with the
+// prover's randomness and the Fiat-Shamir challenges injected (include/ringo.h).
 //
-// Pipeline per batch of B commits (all device-resident, one stream):
+// Commit pipeline per batch of B commits (all device-resident, one stream):
 //   1. digits_kernel   thread per (commit, column, row, slot): source element (v, firstRow =
 //                      v - lastRow shifted, lastRow, mask; prover.go:65-128) -> fromMont ->
-//                      base-b digits (encoder.go:120-146, utils.go:12-19) into the encode's
-//                      coefficient slots j*slots+i.
-//   2. prep_kernel     workgroup per ring polynomial: the randEncode tail (encoder.go:166-200:
+//                      base-b digits (encoder.go:120-146, utils.go:12-19), two per long
+//                      division by b^2, into the encode's coefficient slots j*slots+i.
+//   2. prep256_kernel  wave per ring polynomial (d = 256; prep_kernel, a workgroup per
+//                      polynomial, covers other d): the randEncode tail (encoder.go:166-200:
 //                      MForm(noise), X^slots negacyclic shift, - b*s, + MForm(digits)) or the
-//                      MLWE finalize (prover.go:130-141: signed residue, MForm), then the
-//                      d-point negacyclic NTT per RNS limb in LDS (Lattigo ordering/roots).
-//   3. mac_kernel      thread per (commit, column, limb, coeff): the inner Ajtai product
-//                      sum_k In[j][k]*Enc[k] + sum_k CK.MLWE[j][k]*MLWE[k] for every j, kept
-//                      as exact 160-bit sums and reduced once (MulCoeffsMontgomeryThenAdd
-//                      summed == (sum a*b) * 2^-64 mod q), + MLWE[mlwe+j] (prover.go:149-157).
+//                      MLWE finalize (prover.go:130-141), then the 256-point negacyclic NTT per
+//                      RNS limb in registers (Lattigo ordering/roots).
+//   3. mac3_kernel     per-(limb, coeff) modular GEMM for the inner Ajtai product
+//                      sum_k In[j][k]*Enc[k] + sum_k CK.MLWE[j][k]*MLWE[k] + MLWE[mlwe+j]
+//                      (prover.go:149-157): exact sums reduced once (MulCoeffsMontgomeryThenAdd
+//                      summed == (sum a*b) * 2^-64 mod q); mac_kernel is the fallback for
+//                      primes >= 2^60 or J > 16.
 //   4. round_kernel    workgroup per polynomial: IMForm, INTT, centred CRT (Garner, up to 4
 //                      primes), floor shift by the cut, Euclidean mod q', MForm, NTT in the
 //                      destination ring (prover.go:164-176, rns.go:76-114).
-//   5. mac_kernel + round_kernel again for the outer commitment (prover.go:180-202).
+//   5. the MAC + round_kernel again for the outer commitment (prover.go:180-202).
+// Evaluate: every MulCoeffsMontgomeryThenAdd loop is a J = 1 dot product on mac_kernel
+// (rg_jindo_eval_*), plus rns_reduce_kernel after a cross-GPU sum of partial openBatches.
 // All residues are canonical, so results are bit-exact against the reference's Lattigo
 // calls given the same primes (Lattigo conventions restated: see DESIGN.md, "parity").
 #include <algorithm>
