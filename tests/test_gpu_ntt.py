@@ -122,3 +122,23 @@ def test_ntt_2e16_q255_matches_oracle(fields, batch):
     assert (got == cf.ntt_fwd(a, tw)).all()
     assert (T.InvNTTTo(None, got) == a).all()
     assert (T.InvNTTTo(None, a) == cf.ntt_inv(a, twi, ninv)).all()
+
+
+def test_empty_batches_are_noops(fields):
+    """Empty inputs: the reference's loops over zero polynomials / elements do nothing
+    (ntt.go:98-136 over a batch of none, vec.go:9-121 with n = 0). The device entry points
+    must return OK without launching, and leave the output buffer untouched."""
+    import torch
+
+    q = fields["p63"]
+    F = ringo.Field(q)
+    T = ringo.CyclotomicTransformer(F, 1 << 16)
+    dev = torch.device("cuda", 0)
+    sentinel = torch.full((8,), 12345, dtype=torch.int64, device=dev)
+    T.fwd_dev(sentinel, sentinel, 0)
+    T.inv_dev(sentinel, sentinel, 0)
+    L = ringo.lib()
+    ringo._lib.check(L.rg_vec_dev(F.h, ringo.bigpoly._OPS["mul"], sentinel.data_ptr(), sentinel.data_ptr(),
+                                  sentinel.data_ptr(), 0, None))
+    torch.cuda.synchronize()
+    assert (sentinel.cpu() == 12345).all()
