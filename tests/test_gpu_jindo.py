@@ -127,6 +127,17 @@ def test_commit_dev_batch_matches_single():
         assert (outs["mlwe_out"][b].cpu().numpy().view(np.uint64) == want["mlwe"]).all(), b
 
 
+def test_commit_dev_empty_batch_is_noop():
+    """A batch of zero commits returns OK and launches nothing (the output sentinel survives)."""
+    import torch
+    P, q, params = _setup("t10_b1")
+    prv = jindo.NewProver(params, b"Jindo!")
+    s = torch.full((16,), 777, dtype=torch.int64, device="cuda")
+    prv.commit_dev(0, s, 1000, s, s, s, s, s, s, s, s)
+    torch.cuda.synchronize()
+    assert (s.cpu() == 777).all()
+
+
 def test_commit_rank_panic():
     P, q, params = _setup("t10_b1")
     prv = jindo.NewProver(params, b"Jindo!")
