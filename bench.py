@@ -1,7 +1,9 @@
 """bench.py -- NTT / Jindo-commit throughput of libringo on MI355X.
 
-Contract (see task): `python bench.py --gpus N --steps K --warmup W`; for N > 1 it is launched
-by torch.distributed.run, one rank per GPU (RCCL).  Rank 0 prints ONE JSON line.
+Contract (see task): `python bench.py --gpus N --steps K --warmup W`.  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank on one GPU (RCCL); run plainly
+with --gpus N > 1, bench.py starts torch.distributed.run itself as a CHILD process (before any
+GPU call) and exits with its code.  Rank 0 prints ONE JSON line.
 
 Headline (BASELINE.json configs[1]): forward + inverse negacyclic NTT, degree 2^16, the single
 63-bit jindo-modulus prime p = 47104^4 + 1, batch 1024 polynomials per GPU, inputs resident in
@@ -11,17 +13,26 @@ owns its own 1024 polys; no data-path collective).
 
 Secondary lines in the same JSON object (also measured, not the headline value):
   * l4_ntt: the same fwd+inv step at the Jindo default 255-bit prime (configs[3]), batch 64
-  * jindo: device-resident Jindo commits/s at targetN 2^14 (configs[2]) when available
+  * jindo_commit: device-resident Jindo commits/s at targetN 2^14 (configs[2])
+  * jindo_commit_2e16 (+ jindo_evaluate_2e16): the configs[4] shape, 512 commits per GPU
+    (4096 / 8); at N > 1 the commit key is derived on rank 0 and RCCL-broadcast device to device
 
-roofline: for the NTT transform (two LDS-tiled pass kernels per chunk of polys): algorithmic
-bytes = one read + one write of N*8 B per polynomial per transform; achieved = those bytes /
-the transform's duration measured with HIP events on the launch stream over the timed region.
-cpu_baseline: the C restatement (oracle/liboracle.so, OpenMP) timed on this host on a bounded
-sample of the same workload.
+roofline: for the NTT transform (two LDS-tiled pass kernels per transform): algorithmic bytes =
+one read + one write of N*8 B per polynomial per transform; achieved = those bytes / the
+transform's duration measured with HIP events on the launch stream over the timed region.
+traffic / valu: per-line HBM bytes (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE) and VALU
+instruction counts (SQ_INSTS_VALU) from profiles/kernel_counters.json, which
+tools/profile_bench.sh writes for the libringo.so it profiled; reported only when that file's
+library hash equals the library this run loaded (else null, "stale").
+cpu_baseline: the C restatement (oracle/liboracle.so, threads) timed on this host on bounded
+samples of the NTT headline and of the configs[2] Jindo commit.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,6 +45,10 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 P63 = 47104 ** 4 + 1
 Q255 = 0x430D45996B62AFC2D65643D9E6FB65558E9630DC8C3732810000000000000001
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs; sustained shader clock under this load
+VALU_CYCLES = 4.5  # mean issue cost (cycles / wave64 instruction / SIMD) of the half-rate 64-bit
+                   # integer ops these kernels are made of (tools/ubench)
+STEPS_DONE = {}  # line -> steps executed incl. prewarm/warmup (for per-step PMC attribution)
 
 
 def splitmix64(seed, n):
@@ -68,6 +83,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the L=4 / Jindo lines")
     ap.add_argument("--extra", default="l4,j14,j16", help="secondary lines to run: l4, j14, j16 (comma list)")
+    ap.add_argument("--no-ntt", action="store_true", help="skip the headline NTT line (profiling one line)")
+    ap.add_argument("--no-prewarm", action="store_true", help="no time-based prewarm (deterministic step count)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU-only launcher/timing check: gloo ranks, a trivial host step, no GPU, no libringo")
     ap.add_argument("--j14-batch", type=int, default=256, help="commits per GPU per step, configs[2] shape")
     ap.add_argument("--j16-batch", type=int, default=512,
                     help="commits per GPU per step, configs[4] shape (4096 commits / 8 GPUs)")
@@ -96,14 +115,20 @@ class Events:
         return self.e0.elapsed_time(self.e1)
 
 
+PREWARM = [True]
+
+
 def prewarm(torch, fn, seconds=0.3):
     """Untimed: run the step until the GPU has held its sustained clock for a while (the first
     ~20 steps of this integer-multiply-heavy load run 10-30% slower while power management
-    settles; tools/nttlab/pass_lab 'ramp')."""
+    settles; tools/nttlab/pass_lab 'ramp').  Returns the number of steps run."""
+    n = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while PREWARM[0] and time.perf_counter() - t0 < seconds:
         fn()
         torch.cuda.synchronize()
+        n += 1
+    return n
 
 
 def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
@@ -120,9 +145,10 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
         T.fwd_dev(x, x, batch, stream)
         T.inv_dev(x, x, batch, stream)
 
-    prewarm(torch, step)
+    nw = prewarm(torch, step)
     for _ in range(warmup):
         step()
+    STEPS_DONE["ntt" if L == 1 else "l4"] = nw + warmup + steps
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -144,21 +170,17 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
 
 
 def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world, eval_steps=0):
-    """Device-resident batched commits (rg_jindo_commit_dev) at a BASELINE Jindo config.
-    The commit key is derived from the CRS on rank 0 and broadcast once over RCCL (xGMI)."""
+    """Device-resident batched commits (rg_jindo_commit_dev) at a BASELINE Jindo config.  At
+    N > 1 the commit key is derived from the CRS on rank 0 and broadcast ONCE over RCCL (xGMI),
+    device to device into every rank's prover (ringo.shard.broadcast_prover)."""
     from ringo import jindo
-    from ringo.shard import broadcast_commit_key
+    from ringo.shard import broadcast_prover
     P = json.load(open(os.path.join(ROOT, "tests", "golden", "jindo_params.json")))[cfg_name]
     fq = int(P["field_q_hex"], 16)
     params = jindo.Parameters.from_dict(P, fq)
     dev = torch.device("cuda", torch.cuda.current_device())
     if world > 1:
-        if rank == 0:
-            ck = jindo.NewProver(params, b"Jindo!").commit_key()
-        else:
-            ck = tuple(np.zeros(s, np.uint64) for s in params.ck_shapes().values())
-        ck = broadcast_commit_key(ck, dist, device=dev)
-        prv = jindo.Prover(params, ck=ck)
+        prv = broadcast_prover(params, dist, b"Jindo!")
     else:
         prv = jindo.NewProver(params, b"Jindo!")
     L, nv = params.L, params.rank
@@ -185,9 +207,10 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world,
         prv.commit_dev(batch, v, nv, last, mask, en, mn, outs["incom"], outs["enc"], outs["mlwe_out"], outs["com"],
                        stream)
 
-    prewarm(torch, step, 0.2)
+    nw = prewarm(torch, step, 0.2)
     for _ in range(warmup):
         step()
+    STEPS_DONE["j14" if cfg_name == "t14_b1" else "j16"] = nw + warmup + steps
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -204,7 +227,11 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world,
     nm = params.in_msis + params.mlwe
     opening_words = (params.dcmp * params.nqo * params.d + (params.cols + 1) * params.rows * params.nq * params.d +
                      (params.cols + 1) * nm * params.nq * params.d)
-    bytes_per_commit = 8 * (nv * L + opening_words + params.out_msis * params.nq * params.d)
+    # algorithmic bytes: inputs read once (v, lastRow, mask and the injected int64 noise the
+    # samplers would have produced), the Opening and Commitment written once
+    in_words = (nv * L + params.cols * params.slots * L + params.rows * params.slots * L +
+                (params.cols + 1) * params.rows * params.d + (params.cols + 1) * nm * params.d)
+    bytes_per_commit = 8 * (in_words + opening_words + params.out_msis * params.nq * params.d)
     res = dict(wall_s=wall, kernel_ms=ev.total_ms(), commits=batch * steps, bytes_per_commit=bytes_per_commit)
     if eval_steps and P["batch"] > 1:
         res["eval"] = eval_bench(torch, prv, dist, P, params, batch, outs, eval_steps, g, dev, opening_words)
@@ -252,13 +279,51 @@ def eval_bench(torch, prv, dist, P, params, batch, outs, steps, g, dev, opening_
     return dict(ms=ms, openings_per_gpu=batch, bytes_read=8 * opening_words * batch)
 
 
-def traffic_per_ntt():
-    """HBM bytes per transform measured with rocprofv3 --pmc (FETCH_SIZE x2 + WRITE_SIZE, the
-    gfx950 correction), committed in profiles/ntt_traffic.json by tools/profile_bench.sh."""
+def lib_sha256():
+    p = os.path.join(ROOT, "ringo-snark_amd", "lib", "libringo.so")
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "ntt_traffic.json")))["hbm_bytes_per_transform"]
-    except (OSError, KeyError, ValueError):
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()
+    except OSError:
         return None
+
+
+def counters():
+    """profiles/kernel_counters.json (tools/profile_bench.sh -> tools/kernel_counters.py): per
+    bench line, the rocprofv3 PMC totals of that line's kernels over a profiled run and the steps
+    that run executed.  Used only if it was measured on THIS libringo.so."""
+    try:
+        C = json.load(open(os.path.join(ROOT, "profiles", "kernel_counters.json")))
+    except (OSError, ValueError):
+        return None, "profiles/kernel_counters.json missing"
+    if C.get("lib_sha256") != lib_sha256():
+        return None, "stale: profiles/kernel_counters.json was measured on another libringo.so build"
+    return C, C.get("source", "")
+
+
+# the kernels of one step of each line (setup kernels and the Evaluate MACs excluded)
+LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("ntt256_pass",),
+                "j14": ("digits_kernel", "prep256_kernel", "mac3_kernel<", "round_kernel"),
+                "j16": ("digits_kernel", "prep256_kernel", "mac3_kernel<", "round_kernel")}
+
+
+def line_counters(C, line, units_per_step, kernel_ms_per_step):
+    """traffic (HBM bytes per unit) and the VALU issue block for one line, or None."""
+    if C is None or line not in C.get("lines", {}):
+        return None, None
+    Lc = C["lines"][line]
+    steps = Lc["steps"]
+    ks = [v for n, v in Lc["kernels"].items() if any(p in n for p in LINE_KERNELS[line])]
+    fetch = sum(k.get("FETCH_SIZE", 0.0) for k in ks)  # KiB, summed over dispatches
+    write = sum(k.get("WRITE_SIZE", 0.0) for k in ks)
+    valu = sum(k.get("SQ_INSTS_VALU", 0.0) for k in ks)
+    traffic = (2.0 * fetch + write) * 1024.0 / steps / units_per_step  # gfx950: FETCH_SIZE counts half
+    floor_ms = valu / steps * VALU_CYCLES / (SIMDS * CLOCK_HZ) * 1e3
+    vb = {"insts_per_unit": valu / steps / units_per_step, "cycles_per_inst": VALU_CYCLES, "simds": SIMDS,
+          "clock_ghz": CLOCK_HZ / 1e9, "issue_floor_ms_per_step": floor_ms,
+          "frac": floor_ms / kernel_ms_per_step if kernel_ms_per_step else None,
+          "note": "SQ_INSTS_VALU (wave64 instructions) x cycles/inst / (SIMDs x clock) = the VALU issue floor; "
+                  "frac = floor / measured time (how close this VALU-bound line runs to its instruction roof)"}
+    return traffic, vb
 
 
 def vec_mul_bench(torch, ringo, q, L, n, steps, seed):
@@ -347,13 +412,126 @@ def cpu_baseline(q, L, logn, seconds):
                        "by oracle/oracle.c (C restatement of ntt.go; Go toolchain absent on this host)")
 
 
+def cpu_baseline_jindo(seconds):
+    """The C restatement's whole Commit (oracle.c of_jindo_commit: encode, MLWE, MACs, rounding,
+    outer commit; injected randomness like the GPU line) at the configs[2] shape, one commit per
+    thread at a time (ctypes drops the GIL), on a bounded sample."""
+    from concurrent.futures import ThreadPoolExecutor
+    import coracle as co
+    P = json.load(open(os.path.join(ROOT, "tests", "golden", "jindo_params.json")))["t14_b1"]
+    q = int(P["field_q_hex"], 16)
+    L = (q.bit_length() + 63) // 64
+    cj = co.CJindo(P, q)
+    rng = np.random.default_rng(5)
+    nq, nqo, nm, d = len(P["q"]), len(P["qo"]), P["in_msis"] + P["mlwe"], P["d"]
+    ck = (rng.integers(0, P["q"][0], size=(P["in_msis"], P["rows"], nq, d), dtype=np.uint64),
+          rng.integers(0, P["q"][0], size=(P["in_msis"], P["mlwe"], nq, d), dtype=np.uint64),
+          rng.integers(0, P["qo"][0], size=(P["out_msis"], P["in_com_dcmp_len"], nqo, d), dtype=np.uint64))
+    v = uniform_elems(q, L, P["rank"], 3)
+    last = uniform_elems(q, L, P["cols"] * P["slots"], 4)
+    last[-1] = 0
+    mask = uniform_elems(q, L, P["rows"] * P["slots"], 5).reshape(P["rows"], P["slots"], L)
+    en = rng.integers(-4000, 4000, size=(P["cols"] + 1, P["rows"], d), dtype=np.int64)
+    mn = rng.integers(-40, 40, size=(P["cols"] + 1, nm, d), dtype=np.int64)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+
+    def worker(_):
+        n = 0
+        while time.perf_counter() - t0 < seconds:
+            cj.commit(ck[0], ck[1], ck[2], v, last, mask, en, mn)
+            n += 1
+        return n
+
+    with ThreadPoolExecutor(threads) as ex:
+        done = sum(ex.map(worker, range(threads)))
+    el = time.perf_counter() - t0
+    return dict(value=done / el, unit="commits/s", cores=threads, kind="port",
+                sample=f"{done} commits (configs[2] shape, targetN 2^14, injected randomness) in {el:.1f} s by "
+                       "oracle/oracle.c of_jindo_commit (C restatement of prover.go/encoder.go/rns.go)")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args):
+    """--gpus N without torch.distributed.run around us: start it as a CHILD process (one rank per
+    GPU, rendezvous on 127.0.0.1) before anything touches the GPU, and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def plumbing(args, world, rank):
+    """--plumbing: the launcher, barrier and max-over-ranks timing on gloo with a trivial host step
+    (no GPU, no libringo).  Proves the rank count the driver's N-GPU run will get."""
+    import torch
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+    x = np.arange(1 << 16, dtype=np.uint64)
+
+    def step():
+        np.bitwise_xor(x, np.uint64(rank + 1), out=x)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        tdist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3 / max(args.steps, 1)
+    ranks = [rank]
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        ms = float(t[0])
+        got = [None] * world
+        tdist.all_gather_object(got, rank)
+        ranks = sorted(got)
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing", "value": world / (ms / 1e3), "unit": "steps/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "ranks": ranks,
+                          "plumbing": True}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+    return 0
+
+
+def reduce_max(torch, dist, *vals):
+    if dist is None:
+        return vals if len(vals) > 1 else vals[0]
+    t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = tuple(float(x) for x in t)
+    return out if len(out) > 1 else out[0]
+
+
 def main():
     args = parse()
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch(args)
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.plumbing:
+        return plumbing(args, world, rank)
+    if args.no_prewarm:
+        PREWARM[0] = False
+    import torch
+
     dist = None
     if world > 1:
         import torch.distributed as tdist
@@ -363,101 +541,101 @@ def main():
     import ringo
 
     ringo.lib().rg_set_device(local)
-    r = ntt_step_bench(torch, ringo, dist, P63, 1, args.batch, args.logn, args.steps, args.warmup,
-                       0x52494E47 + rank)
-    ms_step = r["wall_s"] * 1000.0 / args.steps
-    if dist is not None:
-        t = torch.tensor([ms_step, r["kernel_ms"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms_step, kern_ms = float(t[0]), float(t[1])
-        okt = torch.tensor([0 if r["ok"] else 1], device="cuda")
-        dist.all_reduce(okt)
-        ok = int(okt.item()) == 0
-    else:
-        kern_ms, ok = r["kernel_ms"], r["ok"]
-    value = world * 2 * args.batch / (ms_step / 1000.0)
+    C, csrc = counters()
     N = 1 << args.logn
-    bytes_per_ntt = 2 * N * 8
-    achieved = bytes_per_ntt * r["ntts"] / (kern_ms / 1000.0) / 1e9
-    out = {
-        "metric": "NTTs/sec (fwd+inv negacyclic, degree 2^16, 63-bit prime, batch 1024/GPU)",
-        "value": value,
-        "unit": "NTT/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (SplitMix64 seed 0x52494E47, uniform residues mod p)",
-        "config": {"workload": "configs[1]: fwd+inv negacyclic NTT, N=2^16, p=47104^4+1 (63-bit), "
-                               f"batch {args.batch} polys per GPU, HBM-resident",
-                   "rank": N, "field_bits": 63, "batch_per_gpu": args.batch, "parallelism": f"replicas x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_per_ntt(),
-                     "kernel": "ntt16_pass COL + ROW launches (two 8-stage passes per transform); achieved = "
-                               "algorithmic bytes (1 read + 1 write of N*8 B per transform) / HIP-event time of the "
-                               "timed region on the launch stream",
-                     "bytes_per_unit": bytes_per_ntt,
-                     "traffic_note": "HBM bytes per transform from rocprofv3 PMC (profiles/ntt_traffic.json): the "
-                                     "pass-1 -> pass-2 intermediate makes a round trip, 2x algorithmic"},
-        "selfcheck_fwd_inv_identity": ok,
-    }
+    out = {}
     extra = set() if args.no_extra else set(x for x in args.extra.split(",") if x)
-    if "l4" in extra:
-        r4 = ntt_step_bench(torch, ringo, dist, Q255, 4, 64, args.logn, max(2, args.steps // 2), 1, 7 + rank)
-        ms4 = r4["wall_s"] * 1000.0 / max(2, args.steps // 2)
+    if not args.no_ntt:
+        r = ntt_step_bench(torch, ringo, dist, P63, 1, args.batch, args.logn, args.steps, args.warmup,
+                           0x52494E47 + rank)
+        ms_step, kern_ms = reduce_max(torch, dist, r["wall_s"] * 1000.0 / args.steps, r["kernel_ms"])
+        ok = r["ok"]
         if dist is not None:
-            t = torch.tensor([ms4], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ms4 = float(t[0])
+            okt = torch.tensor([0 if r["ok"] else 1], device="cuda")
+            dist.all_reduce(okt)
+            ok = int(okt.item()) == 0
+        bytes_per_ntt = 2 * N * 8
+        achieved = bytes_per_ntt * r["ntts"] / (kern_ms / 1000.0) / 1e9
+        traffic, vb = line_counters(C, "ntt", 2 * args.batch, kern_ms / args.steps)
+        out.update({
+            "metric": "NTTs/sec (fwd+inv negacyclic, degree 2^16, 63-bit prime, batch 1024/GPU)",
+            "value": world * 2 * args.batch / (ms_step / 1000.0),
+            "unit": "NTT/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (SplitMix64 seed 0x52494E47, uniform residues mod p)",
+            "config": {"workload": "configs[1]: fwd+inv negacyclic NTT, N=2^16, p=47104^4+1 (63-bit), "
+                                   f"batch {args.batch} polys per GPU, HBM-resident",
+                       "rank": N, "field_bits": 63, "batch_per_gpu": args.batch, "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ntt16_pass COL + ROW launches (two 8-stage passes per transform); achieved = "
+                                   "algorithmic bytes (1 read + 1 write of N*8 B per transform) / HIP-event time of "
+                                   "the timed region on the launch stream",
+                         "bytes_per_unit": bytes_per_ntt,
+                         "traffic_note": ("HBM bytes per transform, rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE) of "
+                                          "this libringo.so: " + csrc) if traffic else csrc,
+                         "valu": vb},
+            "selfcheck_fwd_inv_identity": ok,
+        })
+    if "l4" in extra:
+        st4 = max(2, args.steps // 2)
+        r4 = ntt_step_bench(torch, ringo, dist, Q255, 4, 64, args.logn, st4, 1, 7 + rank)
+        ms4, k4 = reduce_max(torch, dist, r4["wall_s"] * 1000.0 / st4, r4["kernel_ms"])
         vm = vec_mul_bench(torch, ringo, Q255, 4, 64 * N, 10, 11 + rank)
+        tr4, vb4 = line_counters(C, "l4", 128, k4 / st4)
         out["l4_ntt"] = {"value": world * 2 * 64 / (ms4 / 1000.0), "unit": "NTT/s",
                          "config": "configs[3]: fwd+inv negacyclic NTT, N=2^16, 255-bit Jindo prime, batch 64/GPU",
                          "kernel": "ntt256_pass (4-limb Montgomery, q = 1 mod 2^64; VALU-bound)",
-                         "achieved_GBs": 2 * N * 32 * r4["ntts"] / (r4["kernel_ms"] / 1000.0) / 1e9,
+                         "achieved_GBs": 2 * N * 32 * r4["ntts"] / (k4 / 1000.0) / 1e9,
+                         "traffic_per_ntt": tr4, "valu": vb4,
                          "selfcheck_fwd_inv_identity": r4["ok"],
                          "pointwise_mul": {"unit": "elements/s", "value": world * vm["elems_per_s"],
                                            "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N},
                          "bigpoly_ops": polyops_bench(torch, ringo, Q255, 4, N, 64, 10, 13 + rank)}
     for cfg, jb, key in (("t14_b1", args.j14_batch, "j14"), ("t16_b4096", args.j16_batch, "j16")):
-        if key in extra:
-            jr = jindo_bench(torch, ringo, dist, cfg, jb, max(2, args.steps // 2), 1, rank, world,
-                             eval_steps=max(2, args.steps // 2))
-            jms = jr["wall_s"] * 1000.0 / max(2, args.steps // 2)
-            if dist is not None:
-                t = torch.tensor([jms], dtype=torch.float64, device="cuda")
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                jms = float(t[0])
-            key = "jindo_commit" if cfg == "t14_b1" else "jindo_commit_2e16"
-            out[key] = {"value": world * jb / (jms / 1000.0), "unit": "commits/s",
-                        "config": ("configs[2]: Jindo commit, targetN 2^14 (jindo_test params), q255" if cfg == "t14_b1"
-                                   else "configs[4] shape: Jindo commit, NewParameters(2^16, 4096), q255"),
-                        "batch_per_gpu": jb, "ms_per_batch": jms,
-                        "achieved_GBs": jr["bytes_per_commit"] * jr["commits"] / (jr["kernel_ms"] / 1000.0) / 1e9,
-                        "bytes_per_commit": jr["bytes_per_commit"],
-                        "randomness": "injected (device-generated integers); host Gaussian sampling not timed"}
-            if "eval" in jr:
-                ems = jr["eval"]["ms"]
-                if dist is not None:
-                    t = torch.tensor([ems], dtype=torch.float64, device="cuda")
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                    ems = float(t[0])
-                out["jindo_evaluate_2e16"] = {
-                    "value": world * jb / (ems / 1000.0), "unit": "openings/s",
-                    "config": "configs[4] shape: Prover.Evaluate device work over the batch (%d openings per GPU): "
-                              "batch combination + RCCL all-reduce of partial openBatches + partial evaluations + "
-                              "responses; challenges injected" % jb,
-                    "ms_per_evaluate": ems, "achieved_GBs": jr["eval"]["bytes_read"] / (ems / 1000.0) / 1e9}
+        if key not in extra:
+            continue
+        js = max(2, args.steps // 2)
+        jr = jindo_bench(torch, ringo, dist, cfg, jb, js, 1, rank, world, eval_steps=js)
+        jms, jk = reduce_max(torch, dist, jr["wall_s"] * 1000.0 / js, jr["kernel_ms"])
+        trj, vbj = line_counters(C, key, jb, jk / js)
+        name = "jindo_commit" if cfg == "t14_b1" else "jindo_commit_2e16"
+        out[name] = {"value": world * jb / (jms / 1000.0), "unit": "commits/s",
+                     "config": ("configs[2]: Jindo commit, targetN 2^14 (jindo_test params), q255" if cfg == "t14_b1"
+                                else "configs[4]: Jindo commit, NewParameters(2^16, 4096), q255, "
+                                     f"{jb} commits per GPU ({world * jb} in the job)"),
+                     "batch_per_gpu": jb, "ms_per_batch": jms, "n_gpus": world,
+                     "achieved_GBs": jr["bytes_per_commit"] * jr["commits"] / (jk / 1000.0) / 1e9,
+                     "bytes_per_commit": jr["bytes_per_commit"], "traffic_per_commit": trj, "valu": vbj,
+                     "randomness": "injected (device-generated integers); sampling not timed"}
+        if "eval" in jr:
+            ems = reduce_max(torch, dist, jr["eval"]["ms"])
+            out["jindo_evaluate_2e16"] = {
+                "value": world * jb / (ems / 1000.0), "unit": "openings/s",
+                "config": "configs[4] shape: Prover.Evaluate device work over the batch (%d openings per GPU): "
+                          "batch combination + RCCL all-reduce of partial openBatches + partial evaluations + "
+                          "responses; challenges injected" % jb,
+                "ms_per_evaluate": ems, "achieved_GBs": jr["eval"]["bytes_read"] / (ems / 1000.0) / 1e9}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(P63, 1, args.logn, args.cpu_seconds)
+        if not args.no_ntt:
+            out["cpu_baseline"] = cpu_baseline(P63, 1, args.logn, args.cpu_seconds)
+        if "j14" in extra:
+            out["cpu_baseline_jindo_commit"] = cpu_baseline_jindo(args.cpu_seconds)
+    out["steps_executed"] = dict(STEPS_DONE)
+    out["libringo_sha256"] = lib_sha256()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

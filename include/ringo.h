@@ -19,7 +19,10 @@
  *  - Return value: RG_OK or a negative rg_status; the library never aborts.  The Go shim
  *    maps the codes to the reference's panics (messages in rg_status_string).
  *  - Handles are immutable after creation and may be shared by threads; each call is
- *    thread-safe (host staging is per call).
+ *    thread-safe (host staging is per call).  A Jindo handle keeps device scratch per HIP
+ *    stream, so concurrent `_dev` calls on different streams never share scratch; calls on
+ *    one stream are ordered by the stream.  A handle belongs to the device that was current
+ *    when it was created (RG_ERR_INVALID elsewhere); one handle per GPU.
  */
 #ifndef RINGO_H
 #define RINGO_H
@@ -159,12 +162,21 @@ typedef struct rg_jindo rg_jindo;
  * ck_out  [out_msis][dcmp][nqo][d] CommitKey.Out  (entities.go:50-61)                 */
 rg_status rg_jindo_create(const rg_jindo_params* p, const uint64_t* ck_in, const uint64_t* ck_mlwe,
                           const uint64_t* ck_out, rg_jindo** out);
+/* Same, with the commit key in DEVICE memory on the current device (e.g. the buffer an RCCL
+ * broadcast of the key landed in): copied device-to-device on `stream`, never
+ * through the host.  Returns after the copy and the key transposition have completed. */
+rg_status rg_jindo_create_dev(const rg_jindo_params* p, const uint64_t* d_ck_in, const uint64_t* d_ck_mlwe,
+                              const uint64_t* d_ck_out, void* stream, rg_jindo** out);
 /* Same, deriving the commit key from the CRS exactly as NewCommitKey does
  * (SHA-384 -> AES-256-CTR -> SampleN, entities.go:21-73, uniform.go:38-95). */
 rg_status rg_jindo_create_from_crs(const rg_jindo_params* p, const uint8_t* crs, size_t crs_len, rg_jindo** out);
 void rg_jindo_destroy(rg_jindo* j);
 /* Copy the commit key out (same layouts as rg_jindo_create). */
 rg_status rg_jindo_commit_key(const rg_jindo* j, uint64_t* ck_in, uint64_t* ck_mlwe, uint64_t* ck_out);
+/* The handle's device-resident commit key (same layouts; valid until rg_jindo_destroy), e.g. as
+ * the source of a cross-GPU broadcast. */
+rg_status rg_jindo_commit_key_dev(const rg_jindo* j, const uint64_t** d_ck_in, const uint64_t** d_ck_mlwe,
+                                  const uint64_t** d_ck_out);
 
 /* Prover.Commit (prover.go:45-62) with the randomness INJECTED so the result is
  * bit-exact against Go given the same draws:
@@ -190,8 +202,18 @@ rg_status rg_jindo_commit_dev(const rg_jindo* j, size_t batch, const uint64_t* d
                               const uint64_t* d_last_row, const uint64_t* d_mask, const int64_t* d_enc_noise,
                               const int64_t* d_mlwe_noise, uint64_t* d_incom, uint64_t* d_enc, uint64_t* d_mlwe,
                               uint64_t* d_com, void* stream);
-/* Bytes of device scratch rg_jindo_commit_dev needs for `batch` commits (allocated and
- * cached inside the handle on first use; exposed for capacity planning). */
+/* The deterministic Ajtai core of Commit (prover.go:144-202) for a Go caller that keeps its own
+ * encoder: from the NTT-domain Opening.Encode [cols+1][rows][nq][d] and Opening.MLWE
+ * [cols+1][in_msis+mlwe][nq][d] (as Go holds them after commitColTo's encode and MLWE loops),
+ * the inner Ajtai MACs, CRT rounding into Opening.InCommit [dcmp][nqo][d] (:144-176) and
+ * outerCommitTo into Commitment.Value [out_msis][nq][d] (:180-202).  `_dev`: `batch` openings
+ * back to back, asynchronous on `stream`. */
+rg_status rg_jindo_commit_core(const rg_jindo* j, const uint64_t* enc, const uint64_t* mlwe, uint64_t* o_incom,
+                               uint64_t* o_com);
+rg_status rg_jindo_commit_core_dev(const rg_jindo* j, size_t batch, const uint64_t* d_enc, const uint64_t* d_mlwe,
+                                   uint64_t* d_incom, uint64_t* d_com, void* stream);
+/* Bytes of device scratch rg_jindo_commit_dev needs for `batch` commits (allocated on first
+ * use and cached inside the handle, one set per stream; exposed for capacity planning). */
 size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
 
 /* Prover.Evaluate (prover.go:205-324), device-resident, with the Fiat-Shamir challenges
@@ -231,6 +253,7 @@ rg_status rg_malloc(void** d_ptr, size_t bytes);
 rg_status rg_free(void* d_ptr);
 rg_status rg_memcpy_h2d(void* d_dst, const void* src, size_t bytes, void* stream);
 rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream);
+rg_status rg_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, void* stream);
 rg_status rg_stream_sync(void* stream);
 rg_status rg_set_device(int device);
 

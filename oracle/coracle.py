@@ -38,6 +38,7 @@ def lib():
         L.of_jindo_eval_batch.argtypes = [ctypes.c_void_p, ctypes.c_long] + [u64p] * 8
         L.of_jindo_eval_partial.argtypes = [ctypes.c_void_p, u64p, u64p, u64p]
         L.of_jindo_eval_respond.argtypes = [ctypes.c_void_p] + [u64p] * 5
+        L.of_jindo_commit_core.argtypes = [ctypes.c_void_p] + [u64p] * 7
     return _LIB
 
 
@@ -222,6 +223,14 @@ class CJindo:
             ptr(o["incom"]), ptr(o["enc"]), ptr(o["mlwe"]), ptr(o["com"]))
         if rc:
             raise ValueError("len(v) > params.rank")
+        return o
+
+    def commit_core(self, ck_in, ck_mlwe, ck_out, enc, mlwe):
+        """The Ajtai core of Commit (prover.go:144-202) from the NTT-domain Opening.Encode/MLWE."""
+        sh = self.shapes()
+        o = {k: np.zeros(sh[k], np.uint64) for k in ("incom", "com")}
+        a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (ck_in, ck_mlwe, ck_out, enc, mlwe)]
+        lib().of_jindo_commit_core(ctypes.c_void_p(self.h), *[ptr(x) for x in a], ptr(o["incom"]), ptr(o["com"]))
         return o
 
     # ---- Prover.Evaluate core (prover.go:205-324), challenges injected ----

@@ -687,54 +687,18 @@ static inline void mac_mont(uint64_t* acc, const uint64_t* a, const uint64_t* b,
   }
 }
 
-/* One commit.  See include/ringo.h rg_jindo_commit for every layout. */
-int of_jindo_commit(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
-                    const uint64_t* v, long nv, const uint64_t* last_row, const uint64_t* mask, const int64_t* enc_noise,
-                    const int64_t* mlwe_noise, uint64_t* o_incom, uint64_t* o_enc, uint64_t* o_mlwe, uint64_t* o_com) {
+/* The deterministic Ajtai core of Commit from the NTT-domain opening: the inner MACs, rounding
+ * and InCommit of every column (prover.go:144-176), then outerCommitTo (:180-202).
+ *   enc [cols+1][rows][nq][d], mlwe [cols+1][in_msis+mlwe][nq][d] -> incom, com */
+int of_jindo_commit_core(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
+                         const uint64_t* o_enc, const uint64_t* o_mlwe, uint64_t* o_incom, uint64_t* o_com) {
   const of_jindo_params* P = &J->P;
-  int L = J->F.L, d = P->d, nq = P->nq, nqo = P->nqo, cs = P->cols * P->slots, nm = P->in_msis + P->mlwe;
-  if (nv > P->rank || nv < 1) return -1;
-  size_t polyq = (size_t)nq * d, polyo = (size_t)nqo * d;
-  uint64_t* first = (uint64_t*)calloc((size_t)cs * L, 8);
-  memcpy(first, v, 8 * L); /* genFirstLastRow (prover.go:74-83) */
-  uint64_t zero[MAXL] = {0};
-  for (int i = 1; i < cs; ++i)
-    f_sub(&J->F, first + (size_t)i * L, i < nv ? v + (size_t)i * L : zero, last_row + (size_t)(i - 1) * L, L);
-  memset(o_enc, 0, 8 * polyq * (size_t)(P->cols + 1) * P->rows);
+  const int d = P->d, nq = P->nq, nqo = P->nqo, nm = P->in_msis + P->mlwe;
+  const size_t polyq = (size_t)nq * d, polyo = (size_t)nqo * d;
   uint64_t* com = (uint64_t*)malloc(8 * polyq);
   for (int i = 0; i <= P->cols; ++i) {
-    const int64_t* en = enc_noise + (size_t)i * P->rows * d;
-    uint64_t* enc = o_enc + (size_t)i * P->rows * polyq;
-    int rs = i * P->slots, re = (i + 1) * P->slots;
-    if (i == P->cols) { /* prover.go:93-115 */
-      rand_encode(J, enc, mask, P->slots, en);
-      for (int j = 1; j < P->rows - 1; ++j) {
-        if ((long)j * cs > nv) break;
-        rand_encode(J, enc + (size_t)j * polyq, mask + (size_t)j * P->slots * L, P->slots, en + (size_t)j * d);
-      }
-      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, mask + (size_t)(P->rows - 1) * P->slots * L, P->slots,
-                  en + (size_t)(P->rows - 1) * d);
-    } else { /* prover.go:116-128 */
-      rand_encode(J, enc, first + (size_t)rs * L, P->slots, en);
-      for (int j = 1; j < P->rows - 1; ++j) {
-        long s0 = (long)j * cs + rs, e0 = (long)j * cs + re;
-        if (s0 > nv) break;
-        long e1 = e0 < nv ? e0 : nv;
-        rand_encode(J, enc + (size_t)j * polyq, v + (size_t)s0 * L, (int)(e1 - s0), en + (size_t)j * d);
-      }
-      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, last_row + (size_t)rs * L, P->slots,
-                  en + (size_t)(P->rows - 1) * d);
-    }
-    uint64_t* ml = o_mlwe + (size_t)i * nm * polyq; /* prover.go:130-142 */
-    for (int j = 0; j < nm; ++j) {
-      const int64_t* mn = mlwe_noise + ((size_t)i * nm + j) * d;
-      for (int l = 0; l < nq; ++l) {
-        const of_subring* S = &J->rq[l];
-        uint64_t* p = ml + (size_t)j * polyq + (size_t)l * d;
-        for (int k = 0; k < d; ++k) p[k] = mulmod(signed_res(mn[k], S->q), S->m, S->q);
-        r_ntt(S, p);
-      }
-    }
+    const uint64_t* enc = o_enc + (size_t)i * P->rows * polyq;
+    const uint64_t* ml = o_mlwe + (size_t)i * nm * polyq;
     for (int j = 0; j < P->in_msis; ++j) { /* prover.go:149-176 */
       for (int l = 0; l < nq; ++l) {
         const of_subring* S = &J->rq[l];
@@ -768,8 +732,59 @@ int of_jindo_commit(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck
   }
   free(oc);
   free(com);
-  free(first);
   return 0;
+}
+
+/* One commit.  See include/ringo.h rg_jindo_commit for every layout. */
+int of_jindo_commit(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
+                    const uint64_t* v, long nv, const uint64_t* last_row, const uint64_t* mask, const int64_t* enc_noise,
+                    const int64_t* mlwe_noise, uint64_t* o_incom, uint64_t* o_enc, uint64_t* o_mlwe, uint64_t* o_com) {
+  const of_jindo_params* P = &J->P;
+  int L = J->F.L, d = P->d, nq = P->nq, cs = P->cols * P->slots, nm = P->in_msis + P->mlwe;
+  if (nv > P->rank || nv < 1) return -1;
+  size_t polyq = (size_t)nq * d;
+  uint64_t* first = (uint64_t*)calloc((size_t)cs * L, 8);
+  memcpy(first, v, 8 * L); /* genFirstLastRow (prover.go:74-83) */
+  uint64_t zero[MAXL] = {0};
+  for (int i = 1; i < cs; ++i)
+    f_sub(&J->F, first + (size_t)i * L, i < nv ? v + (size_t)i * L : zero, last_row + (size_t)(i - 1) * L, L);
+  memset(o_enc, 0, 8 * polyq * (size_t)(P->cols + 1) * P->rows);
+  for (int i = 0; i <= P->cols; ++i) {
+    const int64_t* en = enc_noise + (size_t)i * P->rows * d;
+    uint64_t* enc = o_enc + (size_t)i * P->rows * polyq;
+    int rs = i * P->slots, re = (i + 1) * P->slots;
+    if (i == P->cols) { /* prover.go:93-115 */
+      rand_encode(J, enc, mask, P->slots, en);
+      for (int j = 1; j < P->rows - 1; ++j) {
+        if ((long)j * cs > nv) break;
+        rand_encode(J, enc + (size_t)j * polyq, mask + (size_t)j * P->slots * L, P->slots, en + (size_t)j * d);
+      }
+      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, mask + (size_t)(P->rows - 1) * P->slots * L, P->slots,
+                  en + (size_t)(P->rows - 1) * d);
+    } else { /* prover.go:116-128 */
+      rand_encode(J, enc, first + (size_t)rs * L, P->slots, en);
+      for (int j = 1; j < P->rows - 1; ++j) {
+        long s0 = (long)j * cs + rs, e0 = (long)j * cs + re;
+        if (s0 > nv) break;
+        long e1 = e0 < nv ? e0 : nv;
+        rand_encode(J, enc + (size_t)j * polyq, v + (size_t)s0 * L, (int)(e1 - s0), en + (size_t)j * d);
+      }
+      rand_encode(J, enc + (size_t)(P->rows - 1) * polyq, last_row + (size_t)rs * L, P->slots,
+                  en + (size_t)(P->rows - 1) * d);
+    }
+    uint64_t* ml = o_mlwe + (size_t)i * nm * polyq; /* prover.go:130-142 */
+    for (int j = 0; j < nm; ++j) {
+      const int64_t* mn = mlwe_noise + ((size_t)i * nm + j) * d;
+      for (int l = 0; l < nq; ++l) {
+        const of_subring* S = &J->rq[l];
+        uint64_t* p = ml + (size_t)j * polyq + (size_t)l * d;
+        for (int k = 0; k < d; ++k) p[k] = mulmod(signed_res(mn[k], S->q), S->m, S->q);
+        r_ntt(S, p);
+      }
+    }
+  }
+  free(first);
+  return of_jindo_commit_core(J, ck_in, ck_mlwe, ck_out, o_enc, o_mlwe, o_incom, o_com);
 }
 
 /* ------------------------------------------------------------------------------------------ */

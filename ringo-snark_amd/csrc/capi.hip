@@ -75,6 +75,10 @@ rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream
   RG_HIP(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, as_stream(stream)));
   return RG_OK;
 }
+rg_status rg_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, void* stream) {
+  RG_HIP(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, as_stream(stream)));
+  return RG_OK;
+}
 rg_status rg_stream_sync(void* stream) {
   RG_HIP(hipStreamSynchronize(as_stream(stream)));
   return RG_OK;

@@ -28,6 +28,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -265,13 +267,23 @@ struct PrepArgs {
   const uint32_t* digits;     // [B][cols+1][rows][d]
   const long long* enc_noise;  // [B][cols+1][rows][d]
   const long long* mlwe_noise; // [B][cols+1][nm][d]
-  const uint8_t* skip;         // [cols+1][rows] encodes the reference does not perform
   uint64_t* enc;               // [B][cols+1][rows][nq][d]
   uint64_t* mlwe;              // [B][cols+1][nm][nq][d]
   long long n_enc;             // B * (cols+1) * rows
   long long n_ml;              // B * (cols+1) * (inMSIS + mlwe)
   long long clim;              // |noise| bound for the one-integer encode form: 2^61 / base
 };
+
+// Encodes the reference does not perform (prover.go:101-105, 118-123): data rows j in
+// [1, rows-2] of column i whose first index j*cols*slots (+ i*slots) is past len(v); their
+// Opening.Encode stays zero.  The start index grows with j, so the reference's `break`
+// is the same as testing each row.
+__device__ __forceinline__ bool enc_skipped(const JShape& S, int col, int row) {
+  if (row < 1 || row > S.rows - 2) return false;
+  const long long cs = (long long)S.cols * S.slots;
+  const long long start = row * cs + (col == S.cols ? 0 : (long long)col * S.slots);
+  return start > S.nv;
+}
 
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   __shared__ uint64_t poly[kMaxQ][kMaxD];
@@ -285,7 +297,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     const long long b = job / ((long long)(S.cols + 1) * S.rows);
     const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
     dst = a.enc + job * nq * d;
-    if (a.skip[cr]) {  // reference leaves Opening.Encode[i][j] at zero (prover.go:103-105,121-123)
+    if (enc_skipped(S, cr / S.rows, cr % S.rows)) {  // Opening.Encode[i][j] stays zero
       for (int k = tid; k < nq * d; k += blockDim.x) dst[k] = 0;
       return;
     }
@@ -396,7 +408,7 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
   if (is_enc) {
     const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
     dst = a.enc + job * nq * 256;
-    if (a.skip[cr]) {  // reference leaves Opening.Encode[i][j] at zero (prover.go:103-105,121-123)
+    if (enc_skipped(S, cr / S.rows, cr % S.rows)) {  // Opening.Encode[i][j] stays zero
       for (int k = (int)lane; k < nq * 256; k += 64) dst[k] = 0;
       return;
     }
@@ -845,19 +857,29 @@ static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
   return check_launch("jindo mac3");
 }
 
-// host: the commit key of one MAC, split and transposed for mac3_kernel:
+// the commit key of one MAC, split and transposed for mac3_kernel (on the device):
 // out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J zero)
-static std::vector<uint64_t> mac3_key(const std::vector<uint64_t>& A1, int T1, const std::vector<uint64_t>& A2,
-                                      int T2, int J, size_t per_col) {
-  const int JP = mac3_jp(J), T = T1 + T2;
-  std::vector<uint64_t> o(per_col * T * JP, 0);
-  for (size_t lk = 0; lk < per_col; ++lk)
-    for (int t = 0; t < T; ++t)
-      for (int j = 0; j < J; ++j) {
-        const uint64_t x = t < T1 ? A1[((size_t)j * T1 + t) * per_col + lk] : A2[((size_t)j * T2 + (t - T1)) * per_col + lk];
-        o[(lk * T + t) * JP + j] = (x & 0x1fffffffull) | ((x >> 29) << 32);
-      }
-  return o;
+__global__ __launch_bounds__(256) void mac3_key_kernel(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J,
+                                                       int JP, long long per_col, uint64_t* out) {
+  const int T = T1 + T2;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per_col * T * JP) return;
+  const int j = (int)(i % JP);
+  const int t = (int)((i / JP) % T);
+  const long long lk = i / ((long long)JP * T);
+  uint64_t x = 0;
+  if (j < J) x = t < T1 ? A1[((long long)j * T1 + t) * per_col + lk] : A2[((long long)j * T2 + (t - T1)) * per_col + lk];
+  out[i] = (x & 0x1fffffffull) | ((x >> 29) << 32);
+}
+
+static rg_status mac3_key_dev(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J, size_t per_col, DevBuf& out,
+                              hipStream_t st) {
+  const int JP = mac3_jp(J);
+  const long long n = (long long)per_col * (T1 + T2) * JP;
+  RG_TRY(out.alloc((size_t)n * 8));
+  hipLaunchKernelGGL(mac3_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A1, T1, A2, T2, J, JP,
+                     (long long)per_col, out.as<uint64_t>());
+  return check_launch("jindo mac3 key");
 }
 
 // ------------------------------------------------------------------------------------------
@@ -989,21 +1011,27 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
+// Scratch of one commit stream: digits [B][cols+1][rows][d] u32, inner commitments
+// [B][cols+1][inMSIS][nq][d], outer [B][outMSIS][nqo][d].  One per stream, so calls on
+// different streams never share scratch (calls on one stream are ordered by the stream).
+struct rg_jindo_scratch {
+  rg::DevBuf digits, com, ocom;
+};
+
 struct rg_jindo {
   rg_jindo_params p;
   rg_field field;
+  int device = 0;  // the handle's buffers live on this device
   rg::RnsPrime rq[rg::kMaxQ], ro[rg::kMaxQ];
   rg::DevBuf rootsq_f, rootsq_b, rootso_f, rootso_b;
   rg::CrtDev crt_q, crt_o;
   rg::DstDev dst_o;
-  std::vector<uint64_t> h_ck_in, h_ck_mlwe, h_ck_out;
-  rg::DevBuf ck_in, ck_mlwe, ck_out;
-  rg::DevBuf ck3_in, ck3_out;  // commit keys split + transposed for mac3_kernel (inner, outer)
+  rg::DevBuf ck_in, ck_mlwe, ck_out;  // the commit key, device-resident (entities.go:21-73 layouts)
+  rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3_kernel (inner, outer)
   bool mac3_q = false, mac3_o = false;
   uint64_t base_inv;
-  std::mutex mu;  // guards the scratch cache
-  rg::DevBuf s_digits, s_com, s_ocom, s_skip;
-  size_t scratch_batch = 0;
+  std::mutex mu;  // guards `scratch`
+  std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
 };
 
 namespace rg {
@@ -1242,13 +1270,21 @@ static rg_status launch_digits(const rg_jindo* J, size_t batch, const uint64_t* 
   return check_launch("jindo digits");
 }
 
-static rg_status ensure_scratch(rg_jindo* J, size_t batch) {
+// The calling stream's scratch, grown to `batch` commits.  Growing first drains the stream (its
+// earlier commits may still read the old buffers); other streams are untouched.
+static rg_status stream_scratch(rg_jindo* J, size_t batch, hipStream_t st, rg_jindo_scratch** out) {
   const rg_jindo_params& p = J->p;
   const size_t d = p.d;
-  const size_t encs = batch * (p.cols + 1) * p.rows;
-  RG_TRY(J->s_digits.alloc(encs * d * 4));
-  RG_TRY(J->s_com.alloc(batch * (p.cols + 1) * p.in_msis * p.nq * d * 8));
-  RG_TRY(J->s_ocom.alloc(batch * p.out_msis * p.nqo * d * 8));
+  std::lock_guard<std::mutex> lk(J->mu);
+  std::unique_ptr<rg_jindo_scratch>& S = J->scratch[st];
+  if (!S) S.reset(new rg_jindo_scratch());
+  const size_t b_dig = batch * (p.cols + 1) * p.rows * d * 4, b_com = batch * (p.cols + 1) * p.in_msis * p.nq * d * 8,
+               b_oc = batch * p.out_msis * p.nqo * d * 8;
+  if (S->digits.bytes < b_dig || S->com.bytes < b_com || S->ocom.bytes < b_oc) RG_HIP(hipStreamSynchronize(st));
+  RG_TRY(S->digits.alloc(b_dig));
+  RG_TRY(S->com.alloc(b_com));
+  RG_TRY(S->ocom.alloc(b_oc));
+  *out = S.get();
   return RG_OK;
 }
 
@@ -1288,31 +1324,113 @@ static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
   return a;
 }
 
+// A handle's buffers belong to the device it was created on
+static rg_status on_device(const rg_jindo* J) {
+  int cur = -1;
+  RG_HIP(hipGetDevice(&cur));
+  if (cur != J->device) {
+    set_last_error("rg_jindo handle used on device " + std::to_string(cur) + ", created on " +
+                   std::to_string(J->device));
+    return RG_ERR_INVALID;
+  }
+  return RG_OK;
+}
+
+// The deterministic Ajtai core (prover.go:144-202) over a batch of NTT-domain openings:
+// inner MAC, rounding into Opening.InCommit, outer MAC and rounding into Commitment.Value.
+static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, const uint64_t* d_mlwe,
+                             uint64_t* d_incom, uint64_t* d_com, rg_jindo_scratch* sc, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  const int d = p.d, nq = p.nq, nqo = p.nqo, nm = p.in_msis + p.mlwe;
+  // 3. inner MAC
+  MacArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  ma.d = d;
+  ma.nl = nq;
+  ma.J = p.in_msis;
+  ma.ncols = (long long)batch * (p.cols + 1);
+  ma.T1 = p.rows;
+  ma.A1 = J->ck_in.as<uint64_t>();
+  ma.B1 = d_enc;
+  ma.b1_col = (long long)p.rows * nq * d;
+  ma.b1_term = (long long)nq * d;
+  ma.T2 = p.mlwe;
+  ma.A2 = J->ck_mlwe.as<uint64_t>();
+  ma.B2 = d_mlwe;
+  ma.b2_col = (long long)nm * nq * d;
+  ma.b2_term = (long long)nq * d;
+  ma.C = d_mlwe + (long long)p.mlwe * nq * d;  // MLWE[i][mlwe + j]
+  ma.c_col = (long long)nm * nq * d;
+  ma.c_j = (long long)nq * d;
+  ma.out = sc->com.as<uint64_t>();
+  for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
+  if (J->mac3_q) {
+    RG_TRY(launch_mac3(mac3_args(ma, J->ck3_in.as<uint64_t>(), mac3_fold_period(J->rq, nq)), st));
+  } else {
+    RG_TRY(launch_mac(ma, st));
+  }
+  // 4. inner round -> Opening.InCommit (column i, j -> index i*inMSIS + j)
+  RoundArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  ra.d = d;
+  ra.cut = p.log_in_cut;
+  ra.src = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
+  ra.dst = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
+  ra.crt = J->crt_q;
+  ra.dm = J->dst_o;
+  ra.in = sc->com.as<uint64_t>();
+  ra.out = d_incom;
+  ra.out_stride = (long long)nqo * d;
+  ra.out_rows = nqo;
+  {
+    const long long npoly = (long long)batch * (p.cols + 1) * p.in_msis;  // == batch * dcmp, same order
+    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
+    RG_TRY(check_launch("jindo round(in)"));
+  }
+  // 5. outer MAC + round -> Commitment.Value (ringQ-shaped rows, rows >= nqo zero)
+  MacArgs mo;
+  memset(&mo, 0, sizeof(mo));
+  mo.d = d;
+  mo.nl = nqo;
+  mo.J = p.out_msis;
+  mo.ncols = (long long)batch;
+  mo.T1 = p.dcmp;
+  mo.A1 = J->ck_out.as<uint64_t>();
+  mo.B1 = d_incom;
+  mo.b1_col = (long long)p.dcmp * nqo * d;
+  mo.b1_term = (long long)nqo * d;
+  mo.out = sc->ocom.as<uint64_t>();
+  for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
+  if (J->mac3_o) {
+    RG_TRY(launch_mac3(mac3_args(mo, J->ck3_out.as<uint64_t>(), mac3_fold_period(J->ro, nqo)), st));
+  } else {
+    RG_TRY(launch_mac(mo, st));
+  }
+  RoundArgs ro = ra;
+  ro.cut = p.log_out_cut;
+  ro.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
+  ro.crt = J->crt_o;
+  ro.in = sc->ocom.as<uint64_t>();
+  ro.out = d_com;
+  ro.out_stride = (long long)nq * d;
+  ro.out_rows = nq;
+  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), (size_t)nqo * d * 8, st, ro);
+  RG_TRY(check_launch("jindo round(out)"));
+  return RG_OK;
+}
+
 static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
                             const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
                             uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
   const rg_jindo_params& p = J->p;
   if (nv < 1 || nv > (size_t)p.rank) return RG_ERR_RANK;
   if (batch == 0) return RG_OK;
-  std::lock_guard<std::mutex> lk(J->mu);
-  RG_TRY(ensure_scratch(J, batch));
-  const int d = p.d, nq = p.nq, nqo = p.nqo, nm = p.in_msis + p.mlwe;
-  const long long cs = (long long)p.cols * p.slots;
-  // encodes the reference skips (prover.go:101-105, 118-123) -- same for every commit
-  std::vector<uint8_t> skip((size_t)(p.cols + 1) * p.rows, 0);
-  for (int i = 0; i <= p.cols; ++i)
-    for (int j = 1; j < p.rows - 1; ++j) {
-      const long long start = (i == p.cols) ? j * cs : j * cs + (long long)i * p.slots;
-      if (start > (long long)nv)
-        for (int jj = j; jj < p.rows - 1; ++jj) skip[(size_t)i * p.rows + jj] = 1;
-      if (start > (long long)nv) break;
-    }
-  RG_TRY(J->s_skip.alloc(skip.size()));
-  RG_HIP(hipMemcpyAsync(J->s_skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, st));
-  RG_HIP(hipStreamSynchronize(st));  // `skip` is a stack vector
-
+  RG_TRY(on_device(J));
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(J, batch, st, &sc));
+  const int d = p.d, nq = p.nq, nm = p.in_msis + p.mlwe;
   // 1. digits
-  uint32_t* digits = J->s_digits.as<uint32_t>();
+  uint32_t* digits = sc->digits.as<uint32_t>();
   rg_status s;
   switch (p.field_limbs) {
     case 1: s = launch_digits<1>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
@@ -1329,7 +1447,6 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   pa.digits = digits;
   pa.enc_noise = reinterpret_cast<const long long*>(d_en);
   pa.mlwe_noise = reinterpret_cast<const long long*>(d_mn);
-  pa.skip = J->s_skip.as<uint8_t>();
   pa.enc = d_enc;
   pa.mlwe = d_mlwe;
   pa.n_enc = (long long)batch * (p.cols + 1) * p.rows;
@@ -1352,81 +1469,7 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   }
   RG_TRY(check_launch("jindo prep"));
-  // 3. inner MAC
-  MacArgs ma;
-  memset(&ma, 0, sizeof(ma));
-  ma.d = d;
-  ma.nl = nq;
-  ma.J = p.in_msis;
-  ma.ncols = (long long)batch * (p.cols + 1);
-  ma.T1 = p.rows;
-  ma.A1 = J->ck_in.as<uint64_t>();
-  ma.B1 = d_enc;
-  ma.b1_col = (long long)p.rows * nq * d;
-  ma.b1_term = (long long)nq * d;
-  ma.T2 = p.mlwe;
-  ma.A2 = J->ck_mlwe.as<uint64_t>();
-  ma.B2 = d_mlwe;
-  ma.b2_col = (long long)nm * nq * d;
-  ma.b2_term = (long long)nq * d;
-  ma.C = d_mlwe + (long long)p.mlwe * nq * d;  // MLWE[i][mlwe + j]
-  ma.c_col = (long long)nm * nq * d;
-  ma.c_j = (long long)nq * d;
-  ma.out = J->s_com.as<uint64_t>();
-  for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
-  if (J->mac3_q) {
-    RG_TRY(launch_mac3(mac3_args(ma, J->ck3_in.as<uint64_t>(), mac3_fold_period(J->rq, nq)), st));
-  } else {
-    RG_TRY(launch_mac(ma, st));
-  }
-  // 4. inner round -> Opening.InCommit (column i, j -> index i*inMSIS + j)
-  RoundArgs ra;
-  memset(&ra, 0, sizeof(ra));
-  ra.d = d;
-  ra.cut = p.log_in_cut;
-  ra.src = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
-  ra.dst = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
-  ra.crt = J->crt_q;
-  ra.dm = J->dst_o;
-  ra.in = J->s_com.as<uint64_t>();
-  ra.out = d_incom;
-  ra.out_stride = (long long)nqo * d;
-  ra.out_rows = nqo;
-  {
-    const long long npoly = (long long)batch * (p.cols + 1) * p.in_msis;  // == batch * dcmp, same order
-    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
-    RG_TRY(check_launch("jindo round(in)"));
-  }
-  // 5. outer MAC + round -> Commitment.Value (ringQ-shaped rows, rows >= nqo zero)
-  MacArgs mo;
-  memset(&mo, 0, sizeof(mo));
-  mo.d = d;
-  mo.nl = nqo;
-  mo.J = p.out_msis;
-  mo.ncols = (long long)batch;
-  mo.T1 = p.dcmp;
-  mo.A1 = J->ck_out.as<uint64_t>();
-  mo.B1 = d_incom;
-  mo.b1_col = (long long)p.dcmp * nqo * d;
-  mo.b1_term = (long long)nqo * d;
-  mo.out = J->s_ocom.as<uint64_t>();
-  for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
-  if (J->mac3_o) {
-    RG_TRY(launch_mac3(mac3_args(mo, J->ck3_out.as<uint64_t>(), mac3_fold_period(J->ro, nqo)), st));
-  } else {
-    RG_TRY(launch_mac(mo, st));
-  }
-  RoundArgs ro = ra;
-  ro.cut = p.log_out_cut;
-  ro.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
-  ro.crt = J->crt_o;
-  ro.in = J->s_ocom.as<uint64_t>();
-  ro.out = d_com;
-  ro.out_stride = (long long)nq * d;
-  ro.out_rows = nq;
-  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), (size_t)nqo * d * 8, st, ro);
-  RG_TRY(check_launch("jindo round(out)"));
-  return RG_OK;
+  return commit_core(J, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1532,6 +1575,7 @@ static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** 
   RG_TRY(validate(p));
   *J = new rg_jindo();
   (*J)->p = *p;
+  if (hipGetDevice(&(*J)->device) != hipSuccess) (*J)->device = 0;
   rg_status s = build(*J);
   if (s != RG_OK) {
     delete *J;
@@ -1540,24 +1584,33 @@ static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** 
   return s;
 }
 
-static rg_status upload_ck(rg_jindo* J) {
-  RG_TRY(J->ck_in.upload(J->h_ck_in.data(), J->h_ck_in.size() * 8));
-  if (!J->h_ck_mlwe.empty()) RG_TRY(J->ck_mlwe.upload(J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8));
-  RG_TRY(J->ck_out.upload(J->h_ck_out.data(), J->h_ck_out.size() * 8));
+// The commit key is device-resident from here on: ck_in/ck_mlwe/ck_out hold it in the
+// entities.go layouts; mac3's split + transposed copies are built from them on the device.
+static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
   const rg_jindo_params& p = J->p;
   const bool legacy = getenv("RINGO_JINDO_MAC") && getenv("RINGO_JINDO_MAC")[0] == 'l';  // A/B switch
   const size_t pcq = (size_t)p.nq * p.d, pco = (size_t)p.nqo * p.d;
   J->mac3_q = !legacy && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
   J->mac3_o = !legacy && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
-  if (J->mac3_q) {
-    const std::vector<uint64_t> t = mac3_key(J->h_ck_in, p.rows, J->h_ck_mlwe, p.mlwe, p.in_msis, pcq);
-    RG_TRY(J->ck3_in.upload(t.data(), t.size() * 8));
-  }
-  if (J->mac3_o) {
-    const std::vector<uint64_t> t = mac3_key(J->h_ck_out, p.dcmp, {}, 0, p.out_msis, pco);
-    RG_TRY(J->ck3_out.upload(t.data(), t.size() * 8));
-  }
+  if (J->mac3_q)
+    RG_TRY(mac3_key_dev(J->ck_in.as<uint64_t>(), p.rows, J->ck_mlwe.as<uint64_t>(), p.mlwe, p.in_msis, pcq, J->ck3_in, st));
+  if (J->mac3_o) RG_TRY(mac3_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, pco, J->ck3_out, st));
+  RG_HIP(hipStreamSynchronize(st));
   return RG_OK;
+}
+
+// ck_* host (kind = H2D) or device (kind = D2D) arrays -> the handle's device buffers
+static rg_status take_ck(rg_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
+                         hipMemcpyKind kind, hipStream_t st) {
+  size_t a, b, c;
+  ck_sizes(J->p, &a, &b, &c);
+  RG_TRY(J->ck_in.alloc(a * 8));
+  RG_TRY(J->ck_mlwe.alloc(b * 8));
+  RG_TRY(J->ck_out.alloc(c * 8));
+  RG_HIP(hipMemcpyAsync(J->ck_in.p, ck_in, a * 8, kind, st));
+  if (b) RG_HIP(hipMemcpyAsync(J->ck_mlwe.p, ck_mlwe, b * 8, kind, st));
+  RG_HIP(hipMemcpyAsync(J->ck_out.p, ck_out, c * 8, kind, st));
+  return finish_ck(J, st);
 }
 
 rg_status rg_jindo_create(const rg_jindo_params* p, const uint64_t* ck_in, const uint64_t* ck_mlwe,
@@ -1565,12 +1618,21 @@ rg_status rg_jindo_create(const rg_jindo_params* p, const uint64_t* ck_in, const
   if (!ck_in || !ck_out || (!ck_mlwe && p && p->mlwe)) return RG_ERR_INVALID;
   rg_jindo* J = nullptr;
   RG_TRY(jindo_new(p, out, &J));
-  size_t a, b, c;
-  ck_sizes(J->p, &a, &b, &c);
-  J->h_ck_in.assign(ck_in, ck_in + a);
-  if (b) J->h_ck_mlwe.assign(ck_mlwe, ck_mlwe + b);
-  J->h_ck_out.assign(ck_out, ck_out + c);
-  rg_status s = upload_ck(J);
+  rg_status s = take_ck(J, ck_in, ck_mlwe, ck_out, hipMemcpyHostToDevice, nullptr);
+  if (s != RG_OK) {
+    delete J;
+    return s;
+  }
+  *out = J;
+  return RG_OK;
+}
+
+rg_status rg_jindo_create_dev(const rg_jindo_params* p, const uint64_t* d_ck_in, const uint64_t* d_ck_mlwe,
+                              const uint64_t* d_ck_out, void* stream, rg_jindo** out) {
+  if (!d_ck_in || !d_ck_out || (!d_ck_mlwe && p && p->mlwe)) return RG_ERR_INVALID;
+  rg_jindo* J = nullptr;
+  RG_TRY(jindo_new(p, out, &J));
+  rg_status s = take_ck(J, d_ck_in, d_ck_mlwe, d_ck_out, hipMemcpyDeviceToDevice, as_stream(stream));
   if (s != RG_OK) {
     delete J;
     return s;
@@ -1592,24 +1654,22 @@ rg_status rg_jindo_create_from_crs(const rg_jindo_params* p, const uint8_t* crs,
   }
   size_t a, b, c;
   ck_sizes(P, &a, &b, &c);
-  J->h_ck_in.assign(a, 0);
-  J->h_ck_mlwe.assign(b, 0);
-  J->h_ck_out.assign(c, 0);
+  std::vector<uint64_t> h_in(a), h_ml(b), h_out(c);
   const size_t d = P.d;
   // entities.go:24-61: In, then MLWE, then Out; coefficient-major, limb-minor draws
   for (int i = 0; i < P.in_msis; ++i)
     for (int j = 0; j < P.rows; ++j)
       for (size_t k = 0; k < d; ++k)
-        for (int l = 0; l < P.nq; ++l) J->h_ck_in[(((size_t)i * P.rows + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
+        for (int l = 0; l < P.nq; ++l) h_in[(((size_t)i * P.rows + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
   for (int i = 0; i < P.in_msis; ++i)
     for (int j = 0; j < P.mlwe; ++j)
       for (size_t k = 0; k < d; ++k)
-        for (int l = 0; l < P.nq; ++l) J->h_ck_mlwe[(((size_t)i * P.mlwe + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
+        for (int l = 0; l < P.nq; ++l) h_ml[(((size_t)i * P.mlwe + j) * P.nq + l) * d + k] = u.sample_n(P.q[l]);
   for (int i = 0; i < P.out_msis; ++i)
     for (int j = 0; j < P.dcmp; ++j)
       for (size_t k = 0; k < d; ++k)
-        for (int l = 0; l < P.nqo; ++l) J->h_ck_out[(((size_t)i * P.dcmp + j) * P.nqo + l) * d + k] = u.sample_n(P.qo[l]);
-  rg_status s = upload_ck(J);
+        for (int l = 0; l < P.nqo; ++l) h_out[(((size_t)i * P.dcmp + j) * P.nqo + l) * d + k] = u.sample_n(P.qo[l]);
+  rg_status s = take_ck(J, h_in.data(), h_ml.data(), h_out.data(), hipMemcpyHostToDevice, nullptr);
   if (s != RG_OK) {
     delete J;
     return s;
@@ -1618,13 +1678,27 @@ rg_status rg_jindo_create_from_crs(const rg_jindo_params* p, const uint8_t* crs,
   return RG_OK;
 }
 
-void rg_jindo_destroy(rg_jindo* j) { delete j; }
+void rg_jindo_destroy(rg_jindo* j) {
+  if (j) (void)hipDeviceSynchronize();  // scratch may still be in use by queued commits
+  delete j;
+}
 
 rg_status rg_jindo_commit_key(const rg_jindo* J, uint64_t* ck_in, uint64_t* ck_mlwe, uint64_t* ck_out) {
   if (!J) return RG_ERR_INVALID;
-  if (ck_in) memcpy(ck_in, J->h_ck_in.data(), J->h_ck_in.size() * 8);
-  if (ck_mlwe && !J->h_ck_mlwe.empty()) memcpy(ck_mlwe, J->h_ck_mlwe.data(), J->h_ck_mlwe.size() * 8);
-  if (ck_out) memcpy(ck_out, J->h_ck_out.data(), J->h_ck_out.size() * 8);
+  size_t a, b, c;
+  ck_sizes(J->p, &a, &b, &c);
+  if (ck_in) RG_HIP(hipMemcpy(ck_in, J->ck_in.p, a * 8, hipMemcpyDeviceToHost));
+  if (ck_mlwe && b) RG_HIP(hipMemcpy(ck_mlwe, J->ck_mlwe.p, b * 8, hipMemcpyDeviceToHost));
+  if (ck_out) RG_HIP(hipMemcpy(ck_out, J->ck_out.p, c * 8, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+
+rg_status rg_jindo_commit_key_dev(const rg_jindo* J, const uint64_t** d_ck_in, const uint64_t** d_ck_mlwe,
+                                  const uint64_t** d_ck_out) {
+  if (!J) return RG_ERR_INVALID;
+  if (d_ck_in) *d_ck_in = J->ck_in.as<const uint64_t>();
+  if (d_ck_mlwe) *d_ck_mlwe = J->ck_mlwe.as<const uint64_t>();
+  if (d_ck_out) *d_ck_out = J->ck_out.as<const uint64_t>();
   return RG_OK;
 }
 
@@ -1633,7 +1707,7 @@ size_t rg_jindo_scratch_bytes(const rg_jindo* J, size_t batch) {
   const rg_jindo_params& p = J->p;
   const size_t d = p.d;
   return batch * (p.cols + 1) * p.rows * d * 4 + batch * (p.cols + 1) * p.in_msis * p.nq * d * 8 +
-         batch * p.out_msis * p.nqo * d * 8 + (size_t)(p.cols + 1) * p.rows;
+         batch * p.out_msis * p.nqo * d * 8;
 }
 
 rg_status rg_jindo_commit_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
@@ -1644,6 +1718,38 @@ rg_status rg_jindo_commit_dev(const rg_jindo* J, size_t batch, const uint64_t* d
     return RG_ERR_INVALID;
   return commit_dev(const_cast<rg_jindo*>(J), batch, d_v, nv, d_last, d_mask, d_en, d_mn, d_incom, d_enc, d_mlwe, d_com,
                     as_stream(stream));
+}
+
+rg_status rg_jindo_commit_core_dev(const rg_jindo* J, size_t batch, const uint64_t* d_enc, const uint64_t* d_mlwe,
+                                   uint64_t* d_incom, uint64_t* d_com, void* stream) {
+  if (!J) return RG_ERR_INVALID;
+  if (batch == 0) return RG_OK;
+  if (!d_enc || !d_mlwe || !d_incom || !d_com) return RG_ERR_INVALID;
+  RG_TRY(on_device(J));
+  rg_jindo* Jm = const_cast<rg_jindo*>(J);
+  hipStream_t st = as_stream(stream);
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(Jm, batch, st, &sc));
+  return commit_core(Jm, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
+}
+
+rg_status rg_jindo_commit_core(const rg_jindo* J, const uint64_t* enc, const uint64_t* mlwe, uint64_t* o_incom,
+                               uint64_t* o_com) {
+  if (!J || !enc || !mlwe || !o_incom || !o_com) return RG_ERR_INVALID;
+  const rg_jindo_params& p = J->p;
+  const size_t d = p.d, nm = p.in_msis + p.mlwe;
+  const size_t b_enc = (size_t)(p.cols + 1) * p.rows * p.nq * d * 8, b_ml = (size_t)(p.cols + 1) * nm * p.nq * d * 8;
+  const size_t b_inc = (size_t)p.dcmp * p.nqo * d * 8, b_com = (size_t)p.out_msis * p.nq * d * 8;
+  DevBuf enc_, ml_, inc_, com_;
+  RG_TRY(enc_.upload(enc, b_enc));
+  RG_TRY(ml_.upload(mlwe, b_ml));
+  RG_TRY(inc_.alloc(b_inc));
+  RG_TRY(com_.alloc(b_com));
+  RG_TRY(rg_jindo_commit_core_dev(J, 1, enc_.as<uint64_t>(), ml_.as<uint64_t>(), inc_.as<uint64_t>(),
+                                  com_.as<uint64_t>(), nullptr));
+  RG_HIP(hipMemcpy(o_incom, inc_.p, b_inc, hipMemcpyDeviceToHost));
+  RG_HIP(hipMemcpy(o_com, com_.p, b_com, hipMemcpyDeviceToHost));
+  return RG_OK;
 }
 
 rg_status rg_jindo_commit(const rg_jindo* J, const uint64_t* v, size_t nv, const uint64_t* last_row,

@@ -8,7 +8,7 @@ read like the reference's own tests:
     ev  = NewCyclotomicEvaluator(F, rank)            # bigpoly/cyclotomic.go:15
     p   = ev.NewPoly(False); ev.NTTTo(p, p)          # base_op.go:181
     prv = jindo.NewProver(params, crs)               # jindo/prover.go:28
-    com, open_ = prv.CommitInjected(v, randomness)   # prover.go:45 (randomness injected)
+    com, open_ = prv.Commit(v, randomness)          # prover.go:45 (randomness injected)
 """
 from ._lib import RingoError, lib  # noqa: F401
 from .bigpoly import (CyclicTransformer, CyclotomicTransformer, Field, NewCyclicEvaluator,  # noqa: F401

@@ -66,6 +66,10 @@ _SIGS = {
     "rg_jindo_create": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), u64p, u64p, u64p, ctypes.POINTER(vp)]),
     "rg_jindo_create_from_crs": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.POINTER(vp)]),
+    "rg_jindo_create_dev": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), vp, vp, vp, vp, ctypes.POINTER(vp)]),
+    "rg_jindo_commit_key_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+    "rg_jindo_commit_core": (ctypes.c_int, [vp, u64p, u64p, u64p, u64p]),
+    "rg_jindo_commit_core_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, vp, vp, vp]),
     "rg_jindo_destroy": (None, [vp]),
     "rg_jindo_commit_key": (ctypes.c_int, [vp, u64p, u64p, u64p]),
     "rg_jindo_commit": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u64p, u64p, i64p, i64p, u64p, u64p, u64p, u64p]),
@@ -80,6 +84,7 @@ _SIGS = {
     "rg_free": (ctypes.c_int, [vp]),
     "rg_memcpy_h2d": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
     "rg_memcpy_d2h": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
+    "rg_memcpy_d2d": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp]),
     "rg_set_device": (ctypes.c_int, [ctypes.c_int]),
 }

@@ -19,14 +19,32 @@ class RingoPanic(Exception):
     """Raised where the Go reference panics; str(e) is the reference's message."""
 
 
-def _addr(x):
+_WORD_DTYPES = ("torch.int64", "torch.uint64")
+
+
+def _addr(x, words=None):
+    """Device address of a buffer of 64-bit words.  Tensors must be contiguous, of a 64-bit
+    integer dtype, on the current GPU and (when `words` is given) hold at least that many
+    words; anything else raises RingoPanic instead of letting the kernel read a strided view,
+    another GPU's memory or past the end.  Raw int addresses are taken as they are."""
     if x is None:
         return None
     if isinstance(x, int):
         return x
-    if hasattr(x, "data_ptr"):
-        return x.data_ptr()
-    raise TypeError("device buffer must be a tensor or an int address")
+    if not hasattr(x, "data_ptr"):
+        raise TypeError("device buffer must be a tensor or an int address")
+    if str(x.dtype) not in _WORD_DTYPES:
+        raise RingoPanic(f"device buffer dtype {x.dtype}: need 64-bit words (int64/uint64)")
+    if not x.is_contiguous():
+        raise RingoPanic("device buffer is not contiguous")
+    if x.device.type != "cuda":
+        raise RingoPanic(f"device buffer on {x.device}, need the GPU")
+    import torch
+    if x.device.index != torch.cuda.current_device():
+        raise RingoPanic(f"device buffer on {x.device}, current device is cuda:{torch.cuda.current_device()}")
+    if words is not None and x.numel() < words:
+        raise RingoPanic(f"device buffer holds {x.numel()} words, need {words}")
+    return x.data_ptr()
 
 
 def _stream(s):
@@ -150,10 +168,12 @@ class _Transformer:
         return self._host(lib().rg_ntt_inv, vOut, v)
 
     def fwd_dev(self, d_out, d_in, batch, stream=None):
-        check(lib().rg_ntt_fwd_dev(self.h, _addr(d_out), _addr(d_in), batch, _stream(stream)))
+        w = batch * self.rank * self.field.L
+        check(lib().rg_ntt_fwd_dev(self.h, _addr(d_out, w), _addr(d_in, w), batch, _stream(stream)))
 
     def inv_dev(self, d_out, d_in, batch, stream=None):
-        check(lib().rg_ntt_inv_dev(self.h, _addr(d_out), _addr(d_in), batch, _stream(stream)))
+        w = batch * self.rank * self.field.L
+        check(lib().rg_ntt_inv_dev(self.h, _addr(d_out, w), _addr(d_in, w), batch, _stream(stream)))
 
 
 class CyclotomicTransformer(_Transformer):
@@ -379,4 +399,6 @@ def NewCyclicEvaluator(field, rank):
 
 def vec_dev(field, op, d_out, d_a, d_b, n, stream=None):
     """rg_vec_dev: device-resident pointwise op over n elements."""
-    check(lib().rg_vec_dev(field.h, _OPS[op], _addr(d_out), _addr(d_a), _addr(d_b), n, _stream(stream)))
+    w = n * field.L
+    wb = None if op == "neg" else (field.L if op.startswith("smul") else w)
+    check(lib().rg_vec_dev(field.h, _OPS[op], _addr(d_out, w), _addr(d_a, w), _addr(d_b, wb), n, _stream(stream)))

@@ -110,12 +110,26 @@ class Commitment:  # entities.go:80-82
     Value: np.ndarray
 
 
+def _words(shape):
+    n = 1
+    for x in shape:
+        n *= int(x)
+    return n
+
+
 class Prover:
-    def __init__(self, params, crs=None, ck=None):
+    def __init__(self, params, crs=None, ck=None, ck_dev=None, stream=None):
+        """ck: host arrays (rg_jindo_create); ck_dev: device buffers on the current GPU, e.g. where
+        an RCCL broadcast put the key (rg_jindo_create_dev: copied device-to-device); else the
+        key is derived from `crs` (NewCommitKey, entities.go:21-73)."""
         self.params = params
         h = vp()
         ps = params.c_struct()
-        if ck is not None:
+        if ck_dev is not None:
+            sh = params.ck_shapes()
+            a, b, c = (_addr(x, _words(sh[k])) for x, k in zip(ck_dev, ("ck_in", "ck_mlwe", "ck_out")))
+            st = lib().rg_jindo_create_dev(ctypes.byref(ps), a, b, c, _stream(stream), ctypes.byref(h))
+        elif ck is not None:
             a, b, c = (np.ascontiguousarray(x, np.uint64) for x in ck)
             st = lib().rg_jindo_create(ctypes.byref(ps), ptr(a), ptr(b), ptr(c), ctypes.byref(h))
         else:
@@ -149,11 +163,40 @@ class Prover:
                                     ptr(o["incom"]), ptr(o["enc"]), ptr(o["mlwe_out"]), ptr(o["com"])))
         return Commitment(o["com"]), Opening(o["incom"], o["enc"], o["mlwe_out"])
 
+    def commit_key_dev(self):
+        """Device addresses of the handle's commit key (ck_in, ck_mlwe, ck_out)."""
+        a, b, c = vp(), vp(), vp()
+        check(lib().rg_jindo_commit_key_dev(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
     def commit_dev(self, batch, v, nv, last_row, mask, enc_noise, mlwe_noise, incom, enc, mlwe, com, stream=None):
         """rg_jindo_commit_dev on device buffers (tensors or int addresses)."""
-        check(lib().rg_jindo_commit_dev(self.h, batch, _addr(v), nv, _addr(last_row), _addr(mask), _addr(enc_noise),
-                                        _addr(mlwe_noise), _addr(incom), _addr(enc), _addr(mlwe), _addr(com),
+        sh = self.params.shapes(batch)
+        w = {k: _words(x) for k, x in sh.items()}
+        L = self.params.L
+        check(lib().rg_jindo_commit_dev(self.h, batch, _addr(v, batch * nv * L), nv, _addr(last_row, w["last_row"]),
+                                        _addr(mask, w["mask"]), _addr(enc_noise, w["enc_noise"]),
+                                        _addr(mlwe_noise, w["mlwe_noise"]), _addr(incom, w["incom"]),
+                                        _addr(enc, w["enc"]), _addr(mlwe, w["mlwe_out"]), _addr(com, w["com"]),
                                         _stream(stream)))
+
+    def commit_core(self, enc, mlwe):
+        """The Ajtai core of Commit (prover.go:144-202) from NTT-domain Opening.Encode / MLWE:
+        returns (Commitment.Value, Opening.InCommit)."""
+        sh = self.params.shapes()
+        enc = np.ascontiguousarray(enc, np.uint64)
+        mlwe = np.ascontiguousarray(mlwe, np.uint64)
+        if enc.shape != sh["enc"] or mlwe.shape != sh["mlwe_out"]:
+            raise RingoPanic("inconsistent input(s)")
+        incom, com = np.zeros(sh["incom"], np.uint64), np.zeros(sh["com"], np.uint64)
+        check(lib().rg_jindo_commit_core(self.h, ptr(enc), ptr(mlwe), ptr(incom), ptr(com)))
+        return com, incom
+
+    def commit_core_dev(self, batch, enc, mlwe, incom, com, stream=None):
+        sh = self.params.shapes(batch)
+        check(lib().rg_jindo_commit_core_dev(self.h, batch, _addr(enc, _words(sh["enc"])),
+                                             _addr(mlwe, _words(sh["mlwe_out"])), _addr(incom, _words(sh["incom"])),
+                                             _addr(com, _words(sh["com"])), _stream(stream)))
 
 
     # ---- Prover.Evaluate (jindo/prover.go:205-324), device-resident, challenges injected ----

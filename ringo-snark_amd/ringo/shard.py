@@ -13,13 +13,9 @@ def shard_range(n_units, rank, world):
 
 
 def broadcast_commit_key(ck, dist, device=None, src=0):
-    """Broadcast the three commit-key arrays (uint64, any shape) from `src` to every rank.
-
-    ck: tuple of numpy uint64 arrays on `src` (shapes must be known on every rank: pass
-    zero arrays of the right shape elsewhere).  Uses one flat buffer so the collective is a
-    single large transfer (xGMI links are point-to-point; one big message beats three).
-    Returns the arrays on every rank.
-    """
+    """Host-array variant: broadcast the three commit-key arrays (uint64, any shape) from `src`
+    (zero arrays of the right shape elsewhere) through one flat buffer; returns host arrays.
+    For the throughput path use `broadcast_prover`, which never leaves the GPU."""
     import torch
     sizes = [a.size for a in ck]
     flat = np.concatenate([np.ascontiguousarray(a, np.uint64).reshape(-1) for a in ck])
@@ -33,6 +29,37 @@ def broadcast_commit_key(ck, dist, device=None, src=0):
         res.append(out[off:off + n].reshape(a.shape))
         off += n
     return tuple(res)
+
+
+def broadcast_prover(params, dist, crs, src=0, stream=None):
+    """One jindo.Prover per GPU with ONE collective: rank `src` derives the
+    commit key from the CRS (NewCommitKey, entities.go:21-73), copies it device-to-device into a
+    flat buffer, RCCL broadcasts that buffer over xGMI (one large message: the links are
+    point-to-point), and every other rank builds its prover straight from the received device
+    buffer (rg_jindo_create_dev).  The key never passes through host memory after `src` made it."""
+    import torch
+    from ._lib import check, lib
+    from .jindo import Prover, _words
+    dev = torch.device("cuda", torch.cuda.current_device())
+    sh = params.ck_shapes()
+    n = [_words(sh[k]) for k in ("ck_in", "ck_mlwe", "ck_out")]
+    flat = torch.empty(sum(n), dtype=torch.int64, device=dev)
+    st = None if stream is None else getattr(stream, "cuda_stream", stream)
+    prv = None
+    if dist.get_rank() == src:
+        prv = Prover(params, crs=crs)
+        off = 0
+        for p_src, w in zip(prv.commit_key_dev(), n):
+            if w:
+                check(lib().rg_memcpy_d2d(flat.data_ptr() + 8 * off, p_src, 8 * w, st))
+            off += w
+        check(lib().rg_stream_sync(st))
+    dist.broadcast(flat, src=src)
+    if prv is None:
+        torch.cuda.synchronize()
+        parts = torch.split(flat, n)
+        prv = Prover(params, ck_dev=parts, stream=stream)
+    return prv
 
 
 def allreduce_open_batch(prv, dist, ob_incom, ob_enc, ob_mlwe, stream=None):

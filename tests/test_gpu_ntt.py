@@ -142,3 +142,35 @@ def test_empty_batches_are_noops(fields):
                                   sentinel.data_ptr(), 0, None))
     torch.cuda.synchronize()
     assert (sentinel.cpu() == 12345).all()
+
+
+def test_ntt_2e16_full_batch_spot_check(fields):
+    """The headline's full configs[1] batch (1024 polynomials, 512 MiB, in place as bench.py runs
+    it): polynomials 0, 511 and 1023 of the forward transform against the C oracle, then the
+    inverse restores all 1024 bit-exactly.  Inputs are generated on the device (SplitMix64-like
+    hash of the word index mod p) so the host only materialises the three checked polynomials."""
+    import torch
+    q = fields["p63"]
+    N, B = 1 << 16, 1024
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, _, _ = cf.tables(N)
+    idx = torch.arange(B * N, dtype=torch.int64, device="cuda")
+    z = idx * 0x9E3779B97F4A7C15 + 0x52494E47
+    z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * 0xBF58476D1CE4E5B9
+    z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * 0x94D049BB133111EB
+    z = (z ^ ((z >> 31) & ((1 << 33) - 1))) & ((1 << 62) - 1)
+    x = torch.remainder(z, q)  # < 2^62 < p: already canonical, kept as remainder for clarity
+    picks = [0, 511, 1023]
+    a = np.stack([x[i * N:(i + 1) * N].cpu().numpy().view(np.uint64) for i in picks]).reshape(3, N, 1)
+    ref = x.clone()
+    T.fwd_dev(x, x, B)
+    torch.cuda.synchronize()
+    want = cf.ntt_fwd(a, tw)
+    for j, i in enumerate(picks):
+        got = x[i * N:(i + 1) * N].cpu().numpy().view(np.uint64).reshape(N, 1)
+        assert (got == want[j]).all(), i
+    T.inv_dev(x, x, B)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
