@@ -15,6 +15,7 @@ find $OUT/trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kern
 for line in ntt l4 j14 j16; do
   if [ $line = ntt ]; then LA="--no-extra"; else LA="--no-ntt --extra $line"; fi
   i=0
+  mkdir -p $OUT/pmc/$line
   for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
     i=$((i+1))
     timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc/$line/p$i -o run -- python3 $R/bench.py $LA --no-cpu --no-prewarm --steps 4 --warmup 1 > $OUT/pmc/$line/bench.json 2>$OUT/pmc/$line/p$i.err || { echo "pmc $line pass $i failed"; tail -5 $OUT/pmc/$line/p$i.err; exit 1; }
