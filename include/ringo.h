@@ -216,6 +216,52 @@ rg_status rg_jindo_commit_core_dev(const rg_jindo* j, size_t batch, const uint64
  * use and cached inside the handle, one set per stream; exposed for capacity planning). */
 size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
 
+/* ---- the prover's randomness on the device --------------------- */
+/* The standard deviations jindo.Parameters holds (params.go:99-111): ecdStdDev,
+ * ecdBlindStdDev, maskStdDev, maskBlindStdDev, mlweStdDev, maskMLWEStdDev.  Go takes them from
+ * NewParameters' float search; the library builds the TwinCDT tables (gaussian_twin_cdt.go:13-70),
+ * the ziggurat tables (gaussian_rounded.go:22-52) and the encoder's deltaInv (encoder.go:50-67)
+ * from them.  Setup: call once per handle before the sampled entry points (not concurrently
+ * with them).  All must be > 0 (RoundedGaussianSampler panics otherwise). */
+typedef struct {
+  double ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe;
+} rg_jindo_stddevs;
+rg_status rg_jindo_set_stddevs(rg_jindo* j, const rg_jindo_stddevs* sd);
+/* The encoder's deltaInv[exp] (-b^i / p as Go's big.Float computes it, zeroed below
+ * 2^-50 / (b exp); encoder.go:50-67). */
+rg_status rg_jindo_delta_inv(const rg_jindo* j, double* out);
+
+/* One 32-byte seed per sampler the reference's Commit draws from (each is
+ * NewUniformSamplerWithSeed(seed): key = SHA-384(seed)[:32], IV = [32:48], AES-256-CTR,
+ * uniform.go:38-54): Encoder.twinCDT, Encoder.cosac and the RoundedGaussianSampler inside it,
+ * Prover.mlweSampler, Prover.roundedSampler, and `uniform` in place of crypto/rand for
+ * MustSetRandom (prover.go:65-139, encoder.go:149-183).  A Go caller draws them from crypto/rand.
+ * On the device each sampler instance is a window of its domain's counter space (instance n =
+ * the UniformSampler with IV + n 2^24): one per encode polynomial (twinCDT), per MLWE
+ * polynomial (mlweSampler), per sample (COSAC, rounded) and per field element (uniform),
+ * numbered from `first_commit`, the index of the batch's first commit among all commits made
+ * with these seeds (so batches and GPUs never share keystream).  Each instance is exactly the
+ * reference's sampler; the partition of draws among instances is this library's. */
+typedef struct {
+  uint8_t enc_cdt[32], enc_cosac[32], enc_cosac_round[32], mlwe_cdt[32], mlwe_round[32], uniform[32];
+} rg_jindo_seeds;
+/* The randomness of `batch` commits of v (the layouts rg_jindo_commit_dev takes): lastRow (last
+ * entry 0) and mask elements, the Gaussian samples of every randEncodeTo (centres from deltaInv
+ * and the digits of the encoded elements) and of every MLWE polynomial.  Skipped encodes get 0. */
+rg_status rg_jindo_sample_dev(const rg_jindo* j, size_t batch, const uint64_t* d_v, size_t nv,
+                              const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_last_row,
+                              uint64_t* d_mask, int64_t* d_enc_noise, int64_t* d_mlwe_noise, void* stream);
+/* Prover.Commit end to end on the device (prover.go:45-202): rg_jindo_sample_dev, then
+ * rg_jindo_commit_dev on that randomness (kept in the stream's scratch). */
+rg_status rg_jindo_commit_sampled_dev(const rg_jindo* j, size_t batch, const uint64_t* d_v, size_t nv,
+                                      const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_incom,
+                                      uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream);
+/* UniformSampler.Sample() words [first_word, first_word + n) of instance `instance` of
+ * NewUniformSamplerWithSeed(seed) (instance 0 is that sampler itself; uniform.go:56-82, including
+ * the XOR-accumulating 8192-byte buffer). */
+rg_status rg_uniform_words_dev(const uint8_t* seed, size_t seed_len, unsigned long long instance,
+                               unsigned long long first_word, size_t n, uint64_t* d_out, void* stream);
+
 /* Prover.Evaluate (prover.go:205-324), device-resident, with the Fiat-Shamir challenges
  * INJECTED: the transcript (SHAKE128 over CommitKey/Commitment/Proof serializations),
  * encodeChallengeTo, leftVec/encode and Poly.Evaluate stay in the Go caller, which also keeps

@@ -39,6 +39,11 @@ def lib():
         L.of_jindo_eval_partial.argtypes = [ctypes.c_void_p, u64p, u64p, u64p]
         L.of_jindo_eval_respond.argtypes = [ctypes.c_void_p] + [u64p] * 5
         L.of_jindo_commit_core.argtypes = [ctypes.c_void_p] + [u64p] * 7
+        L.of_jindo_sample.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.c_char_p, ctypes.c_uint64, ctypes.c_long, u64p, ctypes.c_long, u64p, u64p,
+                                      i64p, i64p]
+        L.of_uniform_words.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_long,
+                                       u64p]
     return _LIB
 
 
@@ -233,6 +238,26 @@ class CJindo:
         lib().of_jindo_commit_core(ctypes.c_void_p(self.h), *[ptr(x) for x in a], ptr(o["incom"]), ptr(o["com"]))
         return o
 
+    def sample(self, sd, delta, seeds, first, v):
+        """The randomness of v.shape[0] commits (of_jindo_sample): sd = the six standard deviations
+        (ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe), delta = deltaInv, seeds = 192 bytes."""
+        s = self.ps
+        B, nv = v.shape[0], v.shape[1]
+        nm = s.in_msis + s.mlwe
+        o = dict(last_row=np.zeros((B, s.cols * s.slots, self.L), np.uint64),
+                 mask=np.zeros((B, s.rows, s.slots, self.L), np.uint64),
+                 enc_noise=np.zeros((B, s.cols + 1, s.rows, s.d), np.int64),
+                 mlwe_noise=np.zeros((B, s.cols + 1, nm, s.d), np.int64))
+        sdv = (ctypes.c_double * 6)(*sd)
+        dv = (ctypes.c_double * len(delta))(*delta)
+        vv = np.ascontiguousarray(v, np.uint64)
+        rc = lib().of_jindo_sample(ctypes.c_void_p(self.h), sdv, dv, bytes(seeds), first, B, ptr(vv), nv,
+                                   ptr(o["last_row"]), ptr(o["mask"]), ptr(o["enc_noise"], i64p),
+                                   ptr(o["mlwe_noise"], i64p))
+        if rc:
+            raise RuntimeError("of_jindo_sample: libcrypto unavailable")
+        return o
+
     # ---- Prover.Evaluate core (prover.go:205-324), challenges injected ----
     def eval_shapes(self):
         s = self.ps
@@ -262,3 +287,11 @@ class CJindo:
         a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (ob_enc, ob_mlwe, chals)]
         lib().of_jindo_eval_respond(ctypes.c_void_p(self.h), ptr(a[0]), ptr(a[1]), ptr(a[2]), ptr(pe), ptr(pm))
         return pe, pm
+
+
+def uniform_words(seed, inst, first, n):
+    """UniformSampler.Sample() words [first, first + n) of instance `inst` (oracle.c)."""
+    out = np.zeros(n, np.uint64)
+    if lib().of_uniform_words(bytes(seed), len(seed), inst, first, n, ptr(out)):
+        raise RuntimeError("libcrypto unavailable")
+    return out

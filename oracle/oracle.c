@@ -912,3 +912,350 @@ void of_poly_evaluate(const of_field* F, const uint64_t* p, long n, const uint64
   }
   memcpy(out, z, 8 * (size_t)L);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Samplers (math/csprng) and the randomness Prover.Commit draws (prover.go:65-139,           */
+/* encoder.go:149-183), restated from the Go source over OpenSSL's AES (loaded at run time)    */
+/* with the library's instance layout (include/ringo.h rg_jindo_seeds): instance n of a domain */
+/* is the UniformSampler whose IV is IV + n * 2^24.  Floats: IEEE double, no contraction       */
+/* (built with -ffp-contract=off), glibc libm for exp/log/erfc.                                */
+/* ------------------------------------------------------------------------------------------ */
+#include <dlfcn.h>
+#include <math.h>
+
+typedef struct {
+  unsigned char aes[256]; /* OpenSSL AES_KEY */
+  unsigned char iv[16];
+} of_dom;
+static int (*p_aes_set)(const unsigned char*, int, void*);
+static void (*p_aes_enc)(const unsigned char*, unsigned char*, const void*);
+static unsigned char* (*p_sha384)(const unsigned char*, size_t, unsigned char*);
+static int crypto_load(void) {
+  if (p_aes_enc) return 0;
+  void* h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("libcrypto.so", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return -1;
+  p_aes_set = (int (*)(const unsigned char*, int, void*))dlsym(h, "AES_set_encrypt_key");
+  p_sha384 = (unsigned char* (*)(const unsigned char*, size_t, unsigned char*))dlsym(h, "SHA384");
+  p_aes_enc = (void (*)(const unsigned char*, unsigned char*, const void*))dlsym(h, "AES_encrypt");
+  return (p_aes_set && p_sha384 && p_aes_enc) ? 0 : -1;
+}
+/* NewUniformSamplerWithSeed (uniform.go:38-54) */
+static int dom_init(of_dom* D, const unsigned char* seed, size_t n) {
+  unsigned char r[48];
+  if (crypto_load()) return -1;
+  p_sha384(seed, n, r);
+  memcpy(D->iv, r + 32, 16);
+  return p_aes_set(r, 256, D->aes) == 0 ? 0 : -1;
+}
+typedef struct {
+  const of_dom* D;
+  unsigned char ctr0[16]; /* IV + instance * 2^24 */
+  uint64_t pos;
+} of_uni;
+static void ctr_add(unsigned char c[16], const unsigned char a[16], uint64_t hi, uint64_t lo) {
+  /* c = a + (hi * 2^64 + lo) as 128-bit big-endian */
+  unsigned carry = 0;
+  for (int i = 15; i >= 0; --i) {
+    uint64_t add = i >= 8 ? (lo >> (8 * (15 - i))) & 255 : (hi >> (8 * (7 - i))) & 255;
+    unsigned s = a[i] + (unsigned)add + carry;
+    c[i] = (unsigned char)s;
+    carry = s >> 8;
+  }
+}
+static void uni_init(of_uni* U, const of_dom* D, uint64_t inst) {
+  U->D = D;
+  ctr_add(U->ctr0, D->iv, inst >> 40, inst << 24);
+  U->pos = 0;
+}
+static uint64_t ks_word(const of_uni* U, uint64_t w) { /* word w of the plain keystream */
+  unsigned char ctr[16], out[16];
+  ctr_add(ctr, U->ctr0, 0, w >> 1);
+  p_aes_enc(ctr, out, U->D->aes);
+  uint64_t x = 0;
+  for (int i = 7; i >= 0; --i) x = (x << 8) | out[8 * (w & 1) + i];
+  return x;
+}
+/* Sample() (uniform.go:64-82): buffer chunk c = KS_0 ^ ... ^ KS_c */
+static uint64_t uni_sample(of_uni* U) {
+  uint64_t p = U->pos++, c = p >> 10, o = p & 1023, x = 0;
+  for (uint64_t i = 0; i <= c; ++i) x ^= ks_word(U, (i << 10) + o);
+  return x;
+}
+static double uni_float(of_uni* U) { /* SampleFloat (uniform.go:95-100) */
+  uint64_t r = uni_sample(U) % (1ull << 52);
+  double rf;
+  uint64_t bits = r | ((uint64_t)(1023 + 52) << 52);
+  memcpy(&rf, &bits, 8);
+  return (rf / (double)(1ull << 52)) - 1;
+}
+
+/* computeCDT (gaussian_twin_cdt.go:13-37); Go's amd64 float64->uint64 for x >= 2^63 */
+static uint64_t go_u64(double x) {
+  if (x < 9223372036854775808.0) return (uint64_t)(int64_t)x;
+  double y = x - 9223372036854775808.0;
+  int64_t z = y < 9223372036854775808.0 ? (int64_t)y : INT64_MIN;
+  return (uint64_t)z | 0x8000000000000000ull;
+}
+static int cdt_table(double center, double sigma, uint64_t* t) {
+  int64_t hi = (int64_t)ceil(9 * sigma), lo = -hi;
+  double cdf = 0, norm = sqrt(2 * M_PI) * sigma;
+  int i = 0;
+  for (int64_t x = lo; x <= hi; ++x, ++i) {
+    double xf = (double)x;
+    double rho = exp(-(xf - center) * (xf - center) / (2 * sigma * sigma)) / norm;
+    cdf += rho;
+    t[i] = cdf > 1 ? UINT64_MAX : go_u64(round(cdf * 18446744073709551616.0));
+  }
+  return i;
+}
+static int64_t bsearch_go(const uint64_t* x, int n, uint64_t target, int* found) { /* slices.BinarySearch */
+  int i = 0, j = n;
+  while (i < j) {
+    int h = (int)((unsigned)(i + j) >> 1);
+    if (x[h] < target) i = h + 1; else j = h;
+  }
+  *found = i < n && x[i] == target;
+  return i;
+}
+typedef struct {
+  double sigma;
+  int size;
+  int64_t tail_lo;
+  uint64_t* tables; /* [128][size] */
+} of_cdt;
+static void cdt_init(of_cdt* C, double sigma) {
+  C->sigma = sigma;
+  C->tail_lo = -(int64_t)ceil(9 * sigma);
+  C->size = (int)(-2 * C->tail_lo + 1);
+  C->tables = (uint64_t*)malloc(8 * (size_t)C->size * 128);
+  for (int i = 0; i < 128; ++i) cdt_table((double)i / 128, sigma, C->tables + (size_t)i * C->size);
+}
+/* TwinCDTGaussianSampler.Sample (gaussian_twin_cdt.go:77-112) */
+static int64_t cdt_sample(const of_cdt* C, of_uni* U, double center) {
+  double cFloor = floor(center), cFrac = center - cFloor;
+  int64_t c0 = (int64_t)floor(128 * cFrac) % 128, c1 = (int64_t)ceil(128 * cFrac) % 128;
+  uint64_t u = uni_sample(U);
+  int f;
+  int64_t v0 = bsearch_go(C->tables + c0 * C->size, C->size, u, &f);
+  if (f) v0 -= 1;
+  int64_t v1 = bsearch_go(C->tables + c1 * C->size, C->size, u, &f);
+  if (f) v1 -= 1;
+  if (v0 == v1) return v0 + (int64_t)cFloor + C->tail_lo;
+  double cdf = 0, norm = sqrt(2 * M_PI) * C->sigma;
+  for (int64_t x = C->tail_lo; x <= v0; x++) {
+    double xf = (double)x;
+    cdf += exp(-(xf - cFrac) * (xf - cFrac) / (2 * C->sigma * C->sigma)) / norm;
+  }
+  double p = (double)u / 18446744073709551616.0;
+  if (p < cdf) return v0 + C->tail_lo + (int64_t)cFloor;
+  return v1 + C->tail_lo + (int64_t)cFloor;
+}
+/* ziggurat tables (gaussian_rounded.go:22-52) and normFloat (:77-116) */
+static uint64_t zkn[128];
+static double zwn[128], zfn[128];
+static const double RN = 3.442619855899;
+static double znormal(double x) { return exp(-0.5 * x * x); }
+static void zig_init(void) {
+  double v = RN * znormal(RN) + sqrt(M_PI / 2) * erfc(RN / sqrt(2));
+  double xn[128] = {0};
+  xn[127] = RN;
+  for (int i = 126; i >= 1; i--) xn[i] = sqrt(-2 * log(v / xn[i + 1] + znormal(xn[i + 1])));
+  const double scale = (double)(1ull << 52);
+  for (int i = 1; i < 128; i++) {
+    zkn[i] = go_u64((xn[i - 1] / xn[i]) * scale);
+    zwn[i] = xn[i] / scale;
+    zfn[i] = znormal(xn[i]);
+  }
+  zkn[0] = go_u64((RN * znormal(RN) / v) * scale);
+  zwn[0] = (v / znormal(RN)) / scale;
+  zfn[0] = 0;
+}
+static double norm_float(of_uni* U) {
+  for (;;) {
+    uint64_t r = uni_sample(U);
+    uint64_t b = r >> 63, i = r % (1 << 7), j = (r >> 7) % (1ull << 52);
+    double x = (double)(int64_t)((j ^ -b) + b) * zwn[i];
+    if (j < zkn[i]) return x;
+    if (i == 0) {
+      double u, v;
+      for (;;) {
+        u = -log(uni_float(U)) * (1.0 / RN);
+        v = -log(uni_float(U));
+        if (v + v >= u * u) break;
+      }
+      u += RN;
+      return b == 1 ? -u : u;
+    }
+    double f0 = zfn[i - 1], f1 = zfn[i];
+    if (uni_float(U) * (f0 - f1) < exp(-0.5 * x * x) - f1) return x;
+  }
+}
+/* COSACSampler.Sample (gaussian_cosac.go:22-57) */
+static int64_t cosac_sample(of_uni* base, of_uni* rnd, double center, double stdDev) {
+  double cInt = round(center), cFrac = cInt - center;
+  double r = uni_float(base);
+  if (r < exp(-(cFrac * cFrac) / (2 * stdDev * stdDev)) / (sqrt(2 * M_PI) * stdDev)) return (int64_t)cInt;
+  for (;;) {
+    double y = stdDev * norm_float(rnd);
+    uint64_t b = uni_sample(base) & 1;
+    double yRound;
+    int cmp;
+    if (b == 0) {
+      yRound = round(y) - 1;
+      cmp = yRound <= 0.5;
+    } else {
+      yRound = round(y) + 1;
+      cmp = yRound >= -0.5;
+    }
+    if (cmp) {
+      double rr = uni_float(base);
+      if (rr < exp(-((yRound + cFrac) * (yRound + cFrac) - y * y) / (2 * stdDev * stdDev)))
+        return (int64_t)yRound + (int64_t)cInt;
+    }
+  }
+}
+/* Uint.SetRandom (element.go:299-343) from a sampler instance's bytes */
+static void set_random(const of_field* F, of_uni* U, uint64_t* z) {
+  int L = F->L, bitlen = 0;
+  uint64_t qm1[MAXL];
+  memcpy(qm1, F->q, 8 * L);
+  for (int l = 0; l < L; ++l) if (qm1[l]--) break;
+  for (int l = L - 1; l >= 0; --l) if (qm1[l]) { bitlen = 64 * l + 64 - __builtin_clzll(qm1[l]); break; }
+  int k = (bitlen + 7) / 8, b = bitlen % 8 ? bitlen % 8 : 8;
+  unsigned char bytes[8 * MAXL];
+  uint64_t word = 0;
+  int left = 0;
+  for (;;) {
+    memset(bytes, 0, sizeof(bytes));
+    for (int j = 0; j < k; ++j) {
+      if (!left) { word = uni_sample(U); left = 8; }
+      bytes[j] = (unsigned char)word;
+      word >>= 8;
+      --left;
+    }
+    bytes[k - 1] &= (unsigned char)((1 << b) - 1);
+    for (int l = 0; l < L; ++l) {
+      z[l] = 0;
+      for (int i = 7; i >= 0; --i) z[l] = (z[l] << 8) | bytes[8 * l + i];
+    }
+    if (!geq(z, F->q, L)) return;
+  }
+}
+
+/* The randomness of `batch` commits (layouts: rg_jindo_sample_dev).  sd: ecd, ecd_blind, mask,
+ * mask_blind, mlwe, mask_mlwe; delta: Encoder.deltaInv[exp]; seeds: 6 x 32 bytes in
+ * rg_jindo_seeds order. */
+int of_jindo_sample(const of_jindo* J, const double* sd, const double* delta, const unsigned char* seeds,
+                    uint64_t first, long batch, const uint64_t* v, long nv, uint64_t* o_last, uint64_t* o_mask,
+                    int64_t* o_en, int64_t* o_mn) {
+  const of_jindo_params* P = &J->P;
+  const int L = J->F.L, d = P->d, sl = P->slots, cs = P->cols * P->slots, nm = P->in_msis + P->mlwe;
+  of_dom dom[6];
+  for (int i = 0; i < 6; ++i)
+    if (dom_init(&dom[i], seeds + 32 * i, 32)) return -1;
+  if (!zkn[1] && !zkn[2]) zig_init();
+  of_cdt ce, cm;
+  cdt_init(&ce, sd[0]);
+  cdt_init(&cm, sd[4]);
+  uint64_t* digits = (uint64_t*)malloc(8 * (size_t)d);
+  double* fp = (double*)malloc(8 * (size_t)d);
+  uint64_t* first_row = (uint64_t*)calloc((size_t)cs * L, 8);
+  uint64_t zero[MAXL] = {0};
+  const uint64_t per = (uint64_t)cs + (uint64_t)P->rows * sl;
+  for (long b = 0; b < batch; ++b) {
+    const uint64_t gb = first + (uint64_t)b;
+    const uint64_t* vb = v + (size_t)b * nv * L;
+    uint64_t* last = o_last + (size_t)b * cs * L;
+    uint64_t* mask = o_mask + (size_t)b * P->rows * sl * L;
+    /* MustSetRandom draws: lastRow[0 .. cs-2] (last entry 0), mask rows x slots */
+    for (uint64_t i = 0; i < per; ++i) {
+      uint64_t* dst = i < (uint64_t)cs ? last + i * L : mask + (i - cs) * L;
+      if (i == (uint64_t)cs - 1) { memset(dst, 0, 8 * L); continue; }
+      of_uni U;
+      uni_init(&U, &dom[5], gb * per + i);
+      set_random(&J->F, &U, dst);
+    }
+    memcpy(first_row, vb, 8 * L); /* genFirstLastRow (prover.go:74-83) */
+    for (int i = 1; i < cs; ++i)
+      f_sub(&J->F, first_row + (size_t)i * L, i < nv ? vb + (size_t)i * L : zero, last + (size_t)(i - 1) * L, L);
+    for (int col = 0; col <= P->cols; ++col) {
+      for (int row = 0; row < P->rows; ++row) {
+        int64_t* en = o_en + (((size_t)b * (P->cols + 1) + col) * P->rows + row) * d;
+        const uint64_t* src;
+        int n;
+        double s;
+        if (col == P->cols) { /* prover.go:93-115 */
+          if (row >= 1 && row < P->rows - 1 && (long)row * cs > nv) { memset(en, 0, 8 * (size_t)d); continue; }
+          src = mask + (size_t)row * sl * L;
+          n = sl;
+          s = row == 0 ? sd[3] : sd[2];
+        } else { /* prover.go:116-128 */
+          long s0 = (long)row * cs + (long)col * sl, e0 = s0 + sl;
+          if (row == 0) { src = first_row + (size_t)col * sl * L; n = sl; s = sd[1]; }
+          else if (row == P->rows - 1) { src = last + (size_t)col * sl * L; n = sl; s = sd[0]; }
+          else {
+            if (s0 > nv) { memset(en, 0, 8 * (size_t)d); continue; }
+            src = vb + (size_t)s0 * L;
+            n = (int)((e0 < nv ? e0 : nv) - s0);
+            s = sd[0];
+          }
+        }
+        base_encode(J, digits, src, n);
+        /* encoder.go:153-165, literally */
+        for (int k = 0; k < d; ++k) fp[k] = 0;
+        for (int i = 0; i < P->exp; i++) {
+          if (delta[i] == 0) continue;
+          int dd = d - (i + 1) * sl;
+          for (int j = 0, jj = dd; jj < d; j++, jj++) fp[jj] += delta[i] * (double)digits[j];
+          for (int j = d - dd, jj = 0; j < d; j++, jj++) fp[jj] -= delta[i] * (double)digits[j];
+        }
+        const uint64_t gpoly = (gb * (P->cols + 1) + (uint64_t)col) * P->rows + (uint64_t)row;
+        if (s == sd[0]) { /* twinCDT: the encode's instance, one word per sample */
+          of_uni U;
+          uni_init(&U, &dom[0], gpoly);
+          for (int k = 0; k < d; ++k) en[k] = cdt_sample(&ce, &U, -fp[k]);
+        } else {
+          for (int k = 0; k < d; ++k) { /* cosac: an instance per sample for each of its streams */
+            of_uni B, R;
+            uni_init(&B, &dom[1], gpoly * d + k);
+            uni_init(&R, &dom[2], gpoly * d + k);
+            en[k] = cosac_sample(&B, &R, -fp[k], s);
+          }
+        }
+      }
+      for (int j = 0; j < nm; ++j) { /* prover.go:130-139 */
+        int64_t* mn = o_mn + (((size_t)b * (P->cols + 1) + col) * nm + j) * d;
+        const uint64_t gpoly = (gb * (P->cols + 1) + (uint64_t)col) * nm + (uint64_t)j;
+        if (col == P->cols) {
+          for (int k = 0; k < d; ++k) {
+            of_uni U;
+            uni_init(&U, &dom[4], gpoly * d + k);
+            mn[k] = (int64_t)round(0 + norm_float(&U) * sd[5]);
+          }
+        } else {
+          of_uni U;
+          uni_init(&U, &dom[3], gpoly);
+          for (int k = 0; k < d; ++k) mn[k] = cdt_sample(&cm, &U, 0);
+        }
+      }
+    }
+  }
+  free(ce.tables);
+  free(cm.tables);
+  free(digits);
+  free(fp);
+  free(first_row);
+  return 0;
+}
+
+/* UniformSampler.Sample() words [first, first + n) of instance `inst` of the seed's sampler */
+int of_uniform_words(const unsigned char* seed, size_t seed_len, uint64_t inst, uint64_t first, long n, uint64_t* out) {
+  of_dom D;
+  if (dom_init(&D, seed, seed_len)) return -1;
+  of_uni U;
+  uni_init(&U, &D, inst);
+  U.pos = first;
+  for (long i = 0; i < n; ++i) out[i] = uni_sample(&U);
+  return 0;
+}

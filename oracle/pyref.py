@@ -410,26 +410,52 @@ def aes256_ctr_keystream(key, iv, nbytes):
 
 
 class UniformSampler:
-    """NewUniformSamplerWithSeed (uniform.go:38-54): key = SHA-384(seed)[:32], IV = [32:48]."""
+    """NewUniformSamplerWithSeed (uniform.go:38-54): key = SHA-384(seed)[:32], IV = [32:48].
 
-    def __init__(self, seed, chunk=1 << 20):
-        r = hashlib.sha384(seed).digest()
-        self.key, self.iv = r[:32], r[32:48]
-        self.chunk = chunk
-        self.stream = b""
-        self.pos = 0
-        self.generated = 0
+    Sample() (uniform.go:64-82) refills its 8192-byte buffer with
+    `prng.XORKeyStream(buf, buf)`: the new keystream is XORed INTO the previous buffer, so
+    buffer chunk c holds KS_0 ^ KS_1 ^ ... ^ KS_c (KS_i = keystream bytes [8192 i, 8192 (i+1)));
+    only the first 1024 words are plain keystream."""
+    BUF = 8192
 
-    def _refill(self, need):
-        total = max(2 * self.generated, self.pos + need, self.chunk)
-        self.stream = aes256_ctr_keystream(self.key, self.iv, total)
-        self.generated = total
+    def __init__(self, seed=None, key=None, iv=None):
+        if seed is not None:
+            r = hashlib.sha384(seed).digest()
+            key, iv = r[:32], r[32:48]
+        self.key, self.iv = key, iv
+        self.ks = b""
+        self.chunk = 0        # keystream chunks consumed so far
+        self.buf = bytes(self.BUF)
+        self.ptr = self.BUF
 
-    def sample(self):  # uniform.go:64-82 (little-endian u64)
-        if self.pos + 8 > self.generated:
-            self._refill(8)
-        v = int.from_bytes(self.stream[self.pos:self.pos + 8], "little")
-        self.pos += 8
+    def _next_chunk(self):
+        need = (self.chunk + 1) * self.BUF
+        if len(self.ks) < need:
+            self.ks = aes256_ctr_keystream(self.key, self.iv, max(need, 2 * len(self.ks), 1 << 20))
+        k = self.ks[self.chunk * self.BUF:need]
+        if self.chunk:
+            x = int.from_bytes(self.buf, "little") ^ int.from_bytes(k, "little")
+            self.buf = x.to_bytes(self.BUF, "little")
+        else:
+            self.buf = k
+        self.chunk += 1
+        self.ptr = 0
+
+    def read_bytes(self, n):
+        out = b""
+        while len(out) < n:
+            if self.ptr == self.BUF:
+                self._next_chunk()
+            take = min(n - len(out), self.BUF - self.ptr)
+            out += self.buf[self.ptr:self.ptr + take]
+            self.ptr += take
+        return out
+
+    def sample(self):  # uniform.go:64-82 (little-endian u64; bufSize is a multiple of 8)
+        if self.ptr == self.BUF:
+            self._next_chunk()
+        v = int.from_bytes(self.buf[self.ptr:self.ptr + 8], "little")
+        self.ptr += 8
         return v
 
     def sample_n(self, n):  # uniform.go:85-93
@@ -438,6 +464,9 @@ class UniformSampler:
             r = self.sample()
             if r < bound:
                 return r % n
+
+    def sample_float(self):  # uniform.go:95-100: (Sample() mod 2^52) / 2^52, exactly
+        return (self.sample() % (1 << 52)) / float(1 << 52)
 
 
 # --------------------------------------------------------------------------------------------
@@ -770,3 +799,50 @@ def commit(P, F, ck, v_mont, rnd):
         r = round_to(P, P.qo, ringQO, com, P.log_out_cut)
         value.append(r + [[0] * P.d for _ in range(nq - nqo)])
     return value, {"InCommit": incom, "Encode": enc, "MLWE": mlwe}
+
+
+# --------------------------------------------------------------------------------------------
+# Encoder.deltaInv (jindo/encoder.go:50-67) with Go's big.Float semantics, exactly
+# --------------------------------------------------------------------------------------------
+def _bigfloat_round(num, den, prec):
+    """num/den > 0 rounded to `prec` significant bits, nearest even (big.Float's default
+    ToNearestEven); returns (m, e) with value m * 2^e, 2^(prec-1) <= m < 2^prec."""
+    e = num.bit_length() - den.bit_length() - prec
+    while True:
+        D = den << e if e >= 0 else den
+        N = num if e >= 0 else num << -e
+        q, r = divmod(N, D)
+        if q >= 1 << prec:
+            e += 1
+        elif q < 1 << (prec - 1):
+            e -= 1
+        else:
+            break
+    if 2 * r > D or (2 * r == D and q & 1):
+        q += 1
+        if q == 1 << prec:
+            q >>= 1
+            e += 1
+    return q, e
+
+
+def delta_inv(base, exp):
+    """deltaInv = [-1/p, -b/p, ..., -b^(exp-1)/p], p = b^exp + 1: pFloatInv = Quo(1, pFloat) at
+    prec = bitlen(p), negated, Float64() of each term, then pFloatInv.Mul(pFloatInv, bFloat) (every
+    big.Float result rounded to prec bits); |term| < 2^-50 / (b exp) -> 0 (encoder.go:50-67)."""
+    from fractions import Fraction
+    p = base ** exp + 1
+    prec = p.bit_length()
+    m, e = _bigfloat_round(1, p, prec)
+    thr = math.ldexp(1.0, -50) / (float(base) * float(exp))
+    out = []
+    for _ in range(exp):
+        x = Fraction(m) * (Fraction(2) ** e)
+        d = -float(x)  # Float64(): nearest even
+        if abs(d) < thr:
+            d = 0.0
+        out.append(d)
+        num = m * base
+        m, e2 = _bigfloat_round(num, 1, prec)
+        e += e2
+    return out

@@ -1,8 +1,10 @@
 // ck_crs.hpp -- commit-key derivation from the CRS, exactly as jindo.NewCommitKey does
 // (jindo/entities.go:21-73) on top of math/csprng.UniformSampler (uniform.go:38-95):
 //   key = SHA-384(crs)[0:32], iv = SHA-384(crs)[32:48], AES-256-CTR keystream (128-bit
-//   big-endian counter, Go's cipher.NewCTR), little-endian u64 words, SampleN(q) by
-//   rejection below 2^64-1 - (2^64-1) mod q.
+//   big-endian counter, Go's cipher.NewCTR), little-endian u64 words out of an 8192-byte
+//   buffer that each refill XORs the next keystream chunk INTO (`XORKeyStream(buf, buf)`,
+//   uniform.go:64-70: chunk c holds KS_0 ^ ... ^ KS_c), SampleN(q) by rejection below
+//   2^64-1 - (2^64-1) mod q.
 // SHA-384 and AES come from the system libcrypto, loaded at run time (no OpenSSL headers
 // needed to build; the GPU image ships libcrypto.so.3).  Setup-only, host-side.
 #pragma once
@@ -13,6 +15,17 @@
 #include <vector>
 
 namespace rg {
+
+// SHA-384 from the system libcrypto (NewUniformSamplerWithSeed's key derivation, uniform.go:47)
+inline bool sha384(const uint8_t* m, size_t n, uint8_t out[48]) {
+  void* h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("libcrypto.so", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return false;
+  auto f = (unsigned char* (*)(const unsigned char*, size_t, unsigned char*))dlsym(h, "SHA384");
+  const bool ok = f && f(m, n, out);
+  dlclose(h);
+  return ok;
+}
 
 class CtrStream {
  public:
@@ -56,13 +69,16 @@ class CtrStream {
   }
 
  private:
+  // uniform.go:66-67: s.prng.XORKeyStream(s.buf[:], s.buf[:]) -- the buffer (zero at first)
+  // is encrypted in place, i.e. XORed with the next 8192 keystream bytes
   void refill() {
-    std::vector<unsigned char> zero(1 << 16, 0);
-    buf_.resize(zero.size());
+    buf_.resize(kBuf, 0);
+    std::vector<unsigned char> in(buf_);
     int outl = 0;
-    update_(ctx_, buf_.data(), &outl, zero.data(), (int)zero.size());
+    update_(ctx_, buf_.data(), &outl, in.data(), (int)kBuf);
     pos_ = 0;
   }
+  static constexpr size_t kBuf = 8192;
   void* lib_ = nullptr;
   void* ctx_ = nullptr;
   void* (*ctx_new_)() = nullptr;

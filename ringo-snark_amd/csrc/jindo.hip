@@ -35,6 +35,8 @@
 
 #include "ck_crs.hpp"
 #include "common.hpp"
+#include "csprng.hpp"
+#include "csprng_host.hpp"
 #include "field.hpp"
 #include "host_field.hpp"
 #include "ntt64.hpp"
@@ -1006,6 +1008,197 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
   for (int k = tid; k < a.out_rows * d; k += blockDim.x) out[k] = (k / d < nd) ? poly(k / d)[k % d] : 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// 6. sampling: the randomness Prover.Commit draws (prover.go:65-139, encoder.go:149-183) on the
+// device, from six sampler domains (csprng.hpp: one AES-256-CTR key per domain, a window of
+// the domain's counter space per sampler instance):
+//   kDomEncCdt    Encoder.twinCDT      one instance per encode polynomial (256 words)
+//   kDomCosac     Encoder.cosac        one instance per sample ...
+//   kDomCosacRnd  ... and its RoundedGaussianSampler, one instance per sample
+//   kDomMlweCdt   Prover.mlweSampler   one instance per MLWE polynomial
+//   kDomMlweRnd   Prover.roundedSampler one instance per sample
+//   kDomUniform   crypto/rand (MustSetRandom), one instance per field element
+// Instances are numbered from `first_commit`, the index of the batch's first commit in the
+// prover's sequence, so batches and ranks never share keystream.
+// ------------------------------------------------------------------------------------------
+enum { kDomEncCdt = 0, kDomCosac, kDomCosacRnd, kDomMlweCdt, kDomMlweRnd, kDomUniform, kNumDom };
+
+struct SampleArgs {
+  JShape s;
+  AesKey key[kNumDom];
+  const uint32_t* te0;
+  unsigned long long first_commit;
+  // encode noise
+  const uint32_t* digits;  // [B][cols+1][rows][d]
+  const double* delta;     // deltaInv[exp] (encoder.go:50-67)
+  CdtDev cdt_enc, cdt_mlwe;
+  ZigDev zig;
+  double sd_ecd, sd_ecd_blind, sd_mask, sd_mask_blind, sd_mask_mlwe;
+  long long* enc_noise;   // [B][cols+1][rows][d]
+  long long* mlwe_noise;  // [B][cols+1][nm][d]
+  long long n_enc_pairs, n_ml_pairs;
+};
+
+#pragma clang fp contract(off)
+// centre of coefficient k of one encode: -fpSample[k] (encoder.go:153-165), the deltaInv
+// convolution of the digit polynomial, summed term by term in Go's order
+__device__ __forceinline__ double enc_centre(const SampleArgs& a, const uint32_t* dg, int k) {
+  const JShape& S = a.s;
+  double fp = 0.0;
+  for (int i = 0; i < S.exp; ++i) {
+    const double di = a.delta[i];
+    if (di == 0.0) continue;
+    const int dd = S.d - (i + 1) * S.slots;
+    if (k >= dd)
+      fp = fp + di * (double)dg[k - dd];
+    else
+      fp = fp - di * (double)dg[k + S.d - dd];
+  }
+  return -fp;
+}
+#pragma clang fp contract(on)
+
+// thread = (commit, column, row, coefficient pair): Gaussian samples of one randEncodeTo
+__global__ __launch_bounds__(256) void enc_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  aes_lds_fill(lds, a.te0);
+  __syncthreads();
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.n_enc_pairs) return;
+  const JShape& S = a.s;
+  const int m = (int)(gid % (S.d / 2));
+  const long long poly = gid / (S.d / 2);  // (b, col, row) flattened
+  const int row = (int)(poly % S.rows), col = (int)((poly / S.rows) % (S.cols + 1));
+  long long* out = a.enc_noise + poly * S.d;
+  if (enc_skipped(S, col, row)) {  // the reference draws nothing for these (prover.go:101-105,118-123)
+    out[2 * m] = 0;
+    out[2 * m + 1] = 0;
+    return;
+  }
+  const uint32_t* dg = a.digits + poly * S.d;
+  const double sd = col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
+  const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
+  if (sd == a.sd_ecd) {  // Encoder.twinCDT (encoder.go:169-170): one word per sample
+    uint64_t w0, w1;
+    ks_words(a.key[kDomEncCdt], (gpoly << kWinShift) + (uint64_t)m, lds, w0, w1);
+    out[2 * m] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m), w0);
+    out[2 * m + 1] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m + 1), w1);
+  } else {  // Encoder.cosac (encoder.go:171-172)
+    for (int h = 0; h < 2; ++h) {
+      const int k = 2 * m + h;
+      Uniform base, rnd;
+      base.init(a.key[kDomCosac], lds, gpoly * S.d + k);
+      rnd.init(a.key[kDomCosacRnd], lds, gpoly * S.d + k);
+      out[k] = cosac(a.zig, base, rnd, enc_centre(a, dg, k), sd);
+    }
+  }
+}
+
+// thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
+__global__ __launch_bounds__(256) void mlwe_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  aes_lds_fill(lds, a.te0);
+  __syncthreads();
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.n_ml_pairs) return;
+  const JShape& S = a.s;
+  const int nm = S.in_msis + S.mlwe;
+  const int m = (int)(gid % (S.d / 2));
+  const long long poly = gid / (S.d / 2);  // (b, col, j)
+  const int col = (int)((poly / nm) % (S.cols + 1));
+  long long* out = a.mlwe_noise + poly * S.d;
+  const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * nm + (unsigned long long)poly;
+  if (col != S.cols) {  // mlweSampler.Sample(0): centre 0, one table, no float tail
+    uint64_t w0, w1;
+    ks_words(a.key[kDomMlweCdt], (gpoly << kWinShift) + (uint64_t)m, lds, w0, w1);
+    out[2 * m] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0) + a.cdt_mlwe.tail_lo;
+    out[2 * m + 1] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1) + a.cdt_mlwe.tail_lo;
+  } else {  // roundedSampler.Sample(0, maskMLWEStdDev)
+    for (int h = 0; h < 2; ++h) {
+      const int k = 2 * m + h;
+      Uniform u;
+      u.init(a.key[kDomMlweRnd], lds, gpoly * S.d + k);
+      out[k] = rounded_gauss(a.zig, u, 0.0, a.sd_mask_mlwe);
+    }
+  }
+}
+
+// thread = one MustSetRandom draw: lastRow[0 .. cols*slots-2] (the last entry is zero, not
+// drawn: prover.go:68-72) and the mask column's rows x slots elements (prover.go:93-115).
+// Uint.SetRandom (element.go:299-343): read k = ceil(bitLen/8) bytes, clear the unused top
+// bits, reject while >= q.
+template <int L>
+struct UniArgs {
+  JShape s;
+  AesKey key;
+  const uint32_t* te0;
+  FieldParams<L> F;
+  int kbytes;
+  uint32_t top_mask;
+  unsigned long long first_commit;
+  uint64_t* last_row;  // [B][cols*slots][L]
+  uint64_t* mask;      // [B][rows][slots][L]
+  long long total;     // B * (cols*slots + rows*slots)
+};
+
+template <int L>
+__global__ __launch_bounds__(256) void uniform_elems_kernel(UniArgs<L> a) {
+  __shared__ uint32_t lds[kAesLds];
+  aes_lds_fill(lds, a.te0);
+  __syncthreads();
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.total) return;
+  const JShape& S = a.s;
+  const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
+  const long long b = gid / per, i = gid % per;
+  uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
+  if (i == nl - 1) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) dst[l] = 0;
+    return;
+  }
+  Uniform u;
+  u.init(a.key, lds, (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i);
+  uint64_t word = 0;
+  int left = 0;  // unread bytes of `word`
+  for (;;) {
+    uint64_t z[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) z[l] = 0;
+    for (int j = 0; j < a.kbytes; ++j) {
+      if (!left) {
+        word = u.sample();
+        left = 8;
+      }
+      uint64_t byte = word & 255u;
+      word >>= 8;
+      --left;
+      if (j == a.kbytes - 1) byte &= a.top_mask;
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+        if ((j >> 3) == l) z[l] |= byte << (8 * (j & 7));
+    }
+    if (!geq_q<L>(z, a.F)) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) dst[l] = z[l];
+      return;
+    }
+  }
+}
+
+// raw Sample() words of one UniformSampler instance (rg_uniform_words_dev)
+__global__ __launch_bounds__(256) void uniform_words_kernel(AesKey key, const uint32_t* te0, unsigned long long inst,
+                                                            unsigned long long first, long long n, uint64_t* out) {
+  __shared__ uint32_t lds[kAesLds];
+  aes_lds_fill(lds, te0);
+  __syncthreads();
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  Uniform u;
+  u.init(key, lds, inst);
+  out[gid] = u.word_at(first + (unsigned long long)gid);
+}
 }  // namespace rg
 
 // ------------------------------------------------------------------------------------------
@@ -1016,6 +1209,18 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
 // different streams never share scratch (calls on one stream are ordered by the stream).
 struct rg_jindo_scratch {
   rg::DevBuf digits, com, ocom;
+  rg::DevBuf last, mask, en, mn;  // the sampled randomness of rg_jindo_commit_sampled_dev
+};
+
+// Sampler setup (rg_jindo_set_stddevs): the reference's six standard deviations and the tables
+// derived from them on the host (csprng_host.hpp)
+struct rg_jindo_samplers {
+  bool ready = false;
+  double sd[6];  // ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe
+  rg::DevBuf te0, cdt_enc, cdt_mlwe, zig, delta;
+  int cdt_enc_size = 0, cdt_mlwe_size = 0;
+  int64_t tail_lo_enc = 0, tail_lo_mlwe = 0;
+  std::vector<double> h_delta;
 };
 
 struct rg_jindo {
@@ -1032,6 +1237,7 @@ struct rg_jindo {
   uint64_t base_inv;
   std::mutex mu;  // guards `scratch`
   std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
+  rg_jindo_samplers smp;
 };
 
 namespace rg {
@@ -1419,28 +1625,24 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   return RG_OK;
 }
 
-static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
-                            const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
-                            uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
-  const rg_jindo_params& p = J->p;
-  if (nv < 1 || nv > (size_t)p.rank) return RG_ERR_RANK;
-  if (batch == 0) return RG_OK;
-  RG_TRY(on_device(J));
-  rg_jindo_scratch* sc = nullptr;
-  RG_TRY(stream_scratch(J, batch, st, &sc));
-  const int d = p.d, nq = p.nq, nm = p.in_msis + p.mlwe;
-  // 1. digits
-  uint32_t* digits = sc->digits.as<uint32_t>();
-  rg_status s;
-  switch (p.field_limbs) {
-    case 1: s = launch_digits<1>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
-    case 2: s = launch_digits<2>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
-    case 4: s = launch_digits<4>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
-    case 7: s = launch_digits<7>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
-    default: s = launch_digits<14>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st); break;
+// 1. digits of every encode's source elements into the stream's scratch
+static rg_status digits_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
+                              const uint64_t* d_mask, uint32_t* digits, hipStream_t st) {
+  switch (J->p.field_limbs) {
+    case 1: return launch_digits<1>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st);
+    case 2: return launch_digits<2>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st);
+    case 4: return launch_digits<4>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st);
+    case 7: return launch_digits<7>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st);
+    default: return launch_digits<14>(J, batch, d_v, (long long)nv, d_last, d_mask, digits, st);
   }
-  RG_TRY(s);
-  // 2. prep (encodes + MLWE polys)
+}
+
+// 2.-5. from the digits and the randomness: encode tails + MLWE finalize with their NTTs, then the core
+static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const uint32_t* digits, const int64_t* d_en,
+                                    const int64_t* d_mn, uint64_t* d_incom, uint64_t* d_enc, uint64_t* d_mlwe,
+                                    uint64_t* d_com, rg_jindo_scratch* sc, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  const int d = p.d, nq = p.nq, nm = p.in_msis + p.mlwe;
   PrepArgs pa;
   pa.s = shape_of(p, (long long)nv);
   pa.R = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
@@ -1470,6 +1672,135 @@ static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size
   }
   RG_TRY(check_launch("jindo prep"));
   return commit_core(J, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
+}
+
+static rg_status commit_dev(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const uint64_t* d_last,
+                            const uint64_t* d_mask, const int64_t* d_en, const int64_t* d_mn, uint64_t* d_incom,
+                            uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  if (nv < 1 || nv > (size_t)p.rank) return RG_ERR_RANK;
+  if (batch == 0) return RG_OK;
+  RG_TRY(on_device(J));
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(J, batch, st, &sc));
+  uint32_t* digits = sc->digits.as<uint32_t>();
+  RG_TRY(digits_stage(J, batch, d_v, nv, d_last, d_mask, digits, st));
+  return commit_from_digits(J, batch, nv, digits, d_en, d_mn, d_incom, d_enc, d_mlwe, d_com, sc, st);
+}
+
+// ---- sampling (csprng.hpp) -------------------------------------------------------------
+static rg_status make_keys(const rg_jindo_seeds* seeds, AesKey* keys) {
+  const uint8_t* sd[kNumDom] = {seeds->enc_cdt, seeds->enc_cosac, seeds->enc_cosac_round,
+                                seeds->mlwe_cdt, seeds->mlwe_round, seeds->uniform};
+  for (int i = 0; i < kNumDom; ++i) {
+    uint8_t r[48];
+    if (!sha384(sd[i], 32, r)) {
+      set_last_error("libcrypto SHA384 unavailable");
+      return RG_ERR_UNSUPPORTED;
+    }
+    aes256_expand(r, keys[i].rk);
+    for (int w = 0; w < 4; ++w)
+      keys[i].iv[w] = ((uint32_t)r[32 + 4 * w] << 24) | ((uint32_t)r[33 + 4 * w] << 16) | ((uint32_t)r[34 + 4 * w] << 8) |
+                      r[35 + 4 * w];
+  }
+  return RG_OK;
+}
+
+template <int L>
+static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& key, unsigned long long first,
+                                uint64_t* last, uint64_t* mask, hipStream_t st) {
+  UniArgs<L> a;
+  a.s = shape_of(J->p, 1);
+  a.key = key;
+  a.te0 = J->smp.te0.as<uint32_t>();
+  memcpy(a.F.q, J->field.q, 8 * L);
+  a.F.qinv = J->field.qinv;
+  // element.go:305-318: bitLen of q - 1, k bytes, top-byte mask
+  int bitlen = 0;
+  {
+    uint64_t qm1[16];
+    memcpy(qm1, J->field.q, 8 * L);
+    for (int l = 0; l < L; ++l)
+      if (qm1[l]--) break;
+    for (int l = L - 1; l >= 0; --l)
+      if (qm1[l]) {
+        bitlen = 64 * l + 64 - __builtin_clzll(qm1[l]);
+        break;
+      }
+  }
+  a.kbytes = (bitlen + 7) / 8;
+  const int bb = bitlen % 8 ? bitlen % 8 : 8;
+  a.top_mask = (1u << bb) - 1u;
+  a.first_commit = first;
+  a.last_row = last;
+  a.mask = mask;
+  a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
+  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)((a.total + 255) / 256)), dim3(256), 0, st, a);
+  return check_launch("jindo uniform");
+}
+
+// lastRow/mask (crypto/rand), then digits, then every Gaussian sample of the batch
+static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const rg_jindo_seeds* seeds,
+                              unsigned long long first, uint64_t* d_last, uint64_t* d_mask, int64_t* d_en,
+                              int64_t* d_mn, uint32_t* digits, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  if (!J->smp.ready) {
+    set_last_error("rg_jindo_set_stddevs was not called on this handle");
+    return RG_ERR_INVALID;
+  }
+  SampleArgs a;
+  memset(&a, 0, sizeof(a));
+  RG_TRY(make_keys(seeds, a.key));
+  rg_status s;
+  switch (p.field_limbs) {
+    case 1: s = launch_uniform<1>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+    case 2: s = launch_uniform<2>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+    case 4: s = launch_uniform<4>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+    case 7: s = launch_uniform<7>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+    default: s = launch_uniform<14>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+  }
+  RG_TRY(s);
+  RG_TRY(digits_stage(J, batch, d_v, nv, d_last, d_mask, digits, st));
+  const rg_jindo_samplers& S = J->smp;
+  a.s = shape_of(p, (long long)nv);
+  a.te0 = S.te0.as<uint32_t>();
+  a.first_commit = first;
+  a.digits = digits;
+  a.delta = S.delta.as<double>();
+  a.cdt_enc = CdtDev{S.cdt_enc.as<uint64_t>(), S.cdt_enc_size, S.tail_lo_enc, S.sd[0]};
+  a.cdt_mlwe = CdtDev{S.cdt_mlwe.as<uint64_t>(), S.cdt_mlwe_size, S.tail_lo_mlwe, S.sd[4]};
+  const uint64_t* zg = S.zig.as<uint64_t>();
+  a.zig = ZigDev{zg, reinterpret_cast<const double*>(zg + 128), reinterpret_cast<const double*>(zg + 256)};
+  a.sd_ecd = S.sd[0];
+  a.sd_ecd_blind = S.sd[1];
+  a.sd_mask = S.sd[2];
+  a.sd_mask_blind = S.sd[3];
+  a.sd_mask_mlwe = S.sd[5];
+  a.enc_noise = reinterpret_cast<long long*>(d_en);
+  a.mlwe_noise = reinterpret_cast<long long*>(d_mn);
+  const int nm = p.in_msis + p.mlwe;
+  a.n_enc_pairs = (long long)batch * (p.cols + 1) * p.rows * (p.d / 2);
+  a.n_ml_pairs = (long long)batch * (p.cols + 1) * nm * (p.d / 2);
+  hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 255) / 256)), dim3(256), 0, st, a);
+  RG_TRY(check_launch("jindo enc noise"));
+  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)((a.n_ml_pairs + 255) / 256)), dim3(256), 0, st, a);
+  return check_launch("jindo mlwe noise");
+}
+
+// scratch for the sampled randomness of `batch` commits
+static rg_status sample_scratch(rg_jindo* J, size_t batch, rg_jindo_scratch* sc, hipStream_t st) {
+  const rg_jindo_params& p = J->p;
+  const size_t L = p.field_limbs, d = p.d, nm = p.in_msis + p.mlwe;
+  const size_t bl = batch * p.cols * p.slots * L * 8, bm = batch * p.rows * p.slots * L * 8,
+               be = batch * (p.cols + 1) * p.rows * d * 8, bn = batch * (p.cols + 1) * nm * d * 8;
+  std::lock_guard<std::mutex> lk(J->mu);
+  if (sc->last.bytes < bl || sc->mask.bytes < bm || sc->en.bytes < be || sc->mn.bytes < bn)
+    RG_HIP(hipStreamSynchronize(st));
+  RG_TRY(sc->last.alloc(bl));
+  RG_TRY(sc->mask.alloc(bm));
+  RG_TRY(sc->en.alloc(be));
+  RG_TRY(sc->mn.alloc(bn));
+  return RG_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1781,6 +2112,113 @@ rg_status rg_jindo_commit(const rg_jindo* J, const uint64_t* v, size_t nv, const
   RG_HIP(hipMemcpy(o_enc, enc_.p, b_enc, hipMemcpyDeviceToHost));
   RG_HIP(hipMemcpy(o_mlwe, ml_.p, b_ml, hipMemcpyDeviceToHost));
   RG_HIP(hipMemcpy(o_com, com_.p, b_com, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+
+rg_status rg_jindo_set_stddevs(rg_jindo* J, const rg_jindo_stddevs* sd) {
+  if (!J || !sd) return RG_ERR_INVALID;
+  const double v[6] = {sd->ecd, sd->ecd_blind, sd->mask, sd->mask_blind, sd->mlwe, sd->mask_mlwe};
+  for (double x : v)
+    if (!(x > 0.0) || !std::isfinite(x)) return RG_ERR_INVALID;  // RoundedGaussianSampler panics on <= 0
+  rg_jindo_samplers& S = J->smp;
+  std::lock_guard<std::mutex> lk(J->mu);
+  S.ready = false;
+  memcpy(S.sd, v, sizeof(v));
+  uint32_t te0[256];
+  aes_te0(te0);
+  RG_TRY(S.te0.upload(te0, sizeof(te0)));
+  // Encoder.twinCDT: 128 centre tables at ecdStdDev (twin_cdt.go:48-58); Prover.mlweSampler:
+  // the same at mlweStdDev, of which Sample(0) reads table 0
+  std::vector<uint64_t> enc, ml;
+  for (int c = 0; c < 128; ++c) {
+    const std::vector<uint64_t> t = compute_cdt((double)c / 128.0, v[0]);
+    enc.insert(enc.end(), t.begin(), t.end());
+    S.cdt_enc_size = (int)t.size();
+  }
+  ml = compute_cdt(0.0, v[4]);
+  S.cdt_mlwe_size = (int)ml.size();
+  S.tail_lo_enc = -(int64_t)std::ceil(9.0 * v[0]);
+  S.tail_lo_mlwe = -(int64_t)std::ceil(9.0 * v[4]);
+  RG_TRY(S.cdt_enc.upload(enc.data(), enc.size() * 8));
+  RG_TRY(S.cdt_mlwe.upload(ml.data(), ml.size() * 8));
+  const Ziggurat Z = make_ziggurat();
+  std::vector<uint64_t> zg(384);
+  memcpy(zg.data(), Z.kn, 128 * 8);
+  memcpy(zg.data() + 128, Z.wn, 128 * 8);
+  memcpy(zg.data() + 256, Z.fn, 128 * 8);
+  RG_TRY(S.zig.upload(zg.data(), zg.size() * 8));
+  S.h_delta = compute_delta_inv(J->p.base, J->p.exp);
+  RG_TRY(S.delta.upload(S.h_delta.data(), S.h_delta.size() * 8));
+  S.ready = true;
+  return RG_OK;
+}
+
+rg_status rg_jindo_delta_inv(const rg_jindo* J, double* out) {
+  if (!J || !out) return RG_ERR_INVALID;
+  const std::vector<double> d = compute_delta_inv(J->p.base, J->p.exp);
+  memcpy(out, d.data(), d.size() * 8);
+  return RG_OK;
+}
+
+rg_status rg_jindo_sample_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv,
+                              const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_last_row,
+                              uint64_t* d_mask, int64_t* d_enc_noise, int64_t* d_mlwe_noise, void* stream) {
+  if (!J || !seeds) return RG_ERR_INVALID;
+  if (nv < 1 || nv > (size_t)J->p.rank) return RG_ERR_RANK;
+  if (batch == 0) return RG_OK;
+  if (!d_v || !d_last_row || !d_mask || !d_enc_noise || !d_mlwe_noise) return RG_ERR_INVALID;
+  RG_TRY(on_device(J));
+  rg_jindo* Jm = const_cast<rg_jindo*>(J);
+  hipStream_t st = as_stream(stream);
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(Jm, batch, st, &sc));
+  return sample_stage(Jm, batch, d_v, nv, seeds, first_commit, d_last_row, d_mask, d_enc_noise, d_mlwe_noise,
+                      sc->digits.as<uint32_t>(), st);
+}
+
+rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv,
+                                      const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_incom,
+                                      uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream) {
+  if (!J || !seeds) return RG_ERR_INVALID;
+  if (nv < 1 || nv > (size_t)J->p.rank) return RG_ERR_RANK;
+  if (batch == 0) return RG_OK;
+  if (!d_v || !d_incom || !d_enc || !d_mlwe || !d_com) return RG_ERR_INVALID;
+  RG_TRY(on_device(J));
+  rg_jindo* Jm = const_cast<rg_jindo*>(J);
+  hipStream_t st = as_stream(stream);
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(Jm, batch, st, &sc));
+  RG_TRY(sample_scratch(Jm, batch, sc, st));
+  uint32_t* digits = sc->digits.as<uint32_t>();
+  RG_TRY(sample_stage(Jm, batch, d_v, nv, seeds, first_commit, sc->last.as<uint64_t>(), sc->mask.as<uint64_t>(),
+                      sc->en.as<int64_t>(), sc->mn.as<int64_t>(), digits, st));
+  return commit_from_digits(Jm, batch, nv, digits, sc->en.as<int64_t>(), sc->mn.as<int64_t>(), d_incom, d_enc, d_mlwe,
+                            d_com, sc, st);
+}
+
+rg_status rg_uniform_words_dev(const uint8_t* seed, size_t seed_len, unsigned long long instance,
+                               unsigned long long first_word, size_t n, uint64_t* d_out, void* stream) {
+  if ((!seed && seed_len) || (!d_out && n)) return RG_ERR_INVALID;
+  if (n == 0) return RG_OK;
+  uint8_t r[48];
+  if (!sha384(seed, seed_len, r)) {
+    set_last_error("libcrypto SHA384 unavailable");
+    return RG_ERR_UNSUPPORTED;
+  }
+  AesKey K;
+  aes256_expand(r, K.rk);
+  for (int w = 0; w < 4; ++w)
+    K.iv[w] = ((uint32_t)r[32 + 4 * w] << 24) | ((uint32_t)r[33 + 4 * w] << 16) | ((uint32_t)r[34 + 4 * w] << 8) |
+              r[35 + 4 * w];
+  uint32_t te0[256];
+  aes_te0(te0);
+  DevBuf t;
+  RG_TRY(t.upload(te0, sizeof(te0)));
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(uniform_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, t.as<uint32_t>(),
+                     instance, first_word, (long long)n, d_out);
+  RG_TRY(check_launch("uniform words"));
+  RG_HIP(hipStreamSynchronize(st));  // `t` is freed on return
   return RG_OK;
 }
 

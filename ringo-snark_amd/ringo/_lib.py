@@ -25,6 +25,15 @@ class RingoError(RuntimeError):
         self.message = message
 
 
+class JindoStddevsC(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ["ecd", "ecd_blind", "mask", "mask_blind", "mlwe", "mask_mlwe"]]
+
+
+class JindoSeedsC(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint8 * 32) for n in ["enc_cdt", "enc_cosac", "enc_cosac_round", "mlwe_cdt",
+                                                     "mlwe_round", "uniform"]]
+
+
 class JindoParamsC(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ["rank", "rows", "cols", "slots", "exp", "d", "in_msis", "out_msis", "mlwe", "dcmp",
@@ -71,6 +80,15 @@ _SIGS = {
     "rg_jindo_commit_core": (ctypes.c_int, [vp, u64p, u64p, u64p, u64p]),
     "rg_jindo_commit_core_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, vp, vp, vp]),
     "rg_jindo_destroy": (None, [vp]),
+    "rg_jindo_set_stddevs": (ctypes.c_int, [vp, ctypes.POINTER(JindoStddevsC)]),
+    "rg_jindo_delta_inv": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+    "rg_jindo_sample_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(JindoSeedsC),
+                                           ctypes.c_ulonglong, vp, vp, vp, vp, vp]),
+    "rg_jindo_commit_sampled_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_size_t,
+                                                   ctypes.POINTER(JindoSeedsC), ctypes.c_ulonglong, vp, vp, vp, vp,
+                                                   vp]),
+    "rg_uniform_words_dev": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                                            ctypes.c_size_t, vp, vp]),
     "rg_jindo_commit_key": (ctypes.c_int, [vp, u64p, u64p, u64p]),
     "rg_jindo_commit": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u64p, u64p, i64p, i64p, u64p, u64p, u64p, u64p]),
     "rg_jindo_commit_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -124,7 +142,7 @@ def check(status):
     if status != 0:
         L = lib()
         msg = L.rg_status_string(status).decode()
-        detail = L.rg_last_error().decode() if status == -4 else ""
+        detail = L.rg_last_error().decode() if status in (-1, -3, -4) else ""
         raise RingoError(status, msg, detail)
     return status
 

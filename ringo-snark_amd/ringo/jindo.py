@@ -14,8 +14,40 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import JindoParamsC, check, iptr, lib, ptr, vp
+from ._lib import JindoParamsC, JindoSeedsC, JindoStddevsC, check, iptr, lib, ptr, vp
 from .bigpoly import RingoPanic, _addr, _stream
+
+
+STDDEV_KEYS = ("ecd_sd", "ecd_blind_sd", "mask_sd", "mask_blind_sd", "mlwe_sd", "mask_mlwe_sd")
+
+
+@dataclass
+class Seeds:
+    """One 32-byte seed per sampler Commit draws from (include/ringo.h rg_jindo_seeds)."""
+    enc_cdt: bytes
+    enc_cosac: bytes
+    enc_cosac_round: bytes
+    mlwe_cdt: bytes
+    mlwe_round: bytes
+    uniform: bytes
+
+    @classmethod
+    def derive(cls, master):
+        """Six seeds from one: SHA-256(master || name) (a convenience; Go draws each from crypto/rand)."""
+        import hashlib
+        return cls(**{k: hashlib.sha256(bytes(master) + k.encode()).digest() for k in cls.__dataclass_fields__})
+
+    def raw(self):
+        return b"".join(getattr(self, k) for k in self.__dataclass_fields__)
+
+    def c_struct(self):
+        s = JindoSeedsC()
+        for k in self.__dataclass_fields__:
+            v = getattr(self, k)
+            if len(v) != 32:
+                raise RingoPanic("seed must be 32 bytes")
+            ctypes.memmove(getattr(s, k), v, 32)
+        return s
 
 
 @dataclass
@@ -36,13 +68,15 @@ class Parameters:
     q: list
     qo: list
     field_q: int
+    stddevs: tuple = None  # ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe (params.go:99-111)
 
     @classmethod
     def from_dict(cls, P, field_q):
         return cls(rank=P["rank"], rows=P["rows"], cols=P["cols"], slots=P["slots"], exp=P["exp"], d=P["d"],
                    in_msis=P["in_msis"], out_msis=P["out_msis"], mlwe=P["mlwe"], dcmp=P["in_com_dcmp_len"],
                    log_in_cut=P["log_in_cut"], log_out_cut=P["log_out_cut"], base=P["base"], q=list(P["q"]),
-                   qo=list(P["qo"]), field_q=int(field_q))
+                   qo=list(P["qo"]), field_q=int(field_q),
+                   stddevs=tuple(P[k] for k in STDDEV_KEYS) if all(k in P for k in STDDEV_KEYS) else None)
 
     @property
     def L(self):
@@ -136,6 +170,9 @@ class Prover:
             st = lib().rg_jindo_create_from_crs(ctypes.byref(ps), crs, len(crs), ctypes.byref(h))
         check(st)
         self.h = h
+        if params.stddevs is not None:
+            sd = JindoStddevsC(*params.stddevs)
+            check(lib().rg_jindo_set_stddevs(self.h, ctypes.byref(sd)))
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -179,6 +216,30 @@ class Prover:
                                         _addr(mlwe_noise, w["mlwe_noise"]), _addr(incom, w["incom"]),
                                         _addr(enc, w["enc"]), _addr(mlwe, w["mlwe_out"]), _addr(com, w["com"]),
                                         _stream(stream)))
+
+    def delta_inv(self):
+        """Encoder.deltaInv (encoder.go:50-67) as the library computes it."""
+        out = (ctypes.c_double * self.params.exp)()
+        check(lib().rg_jindo_delta_inv(self.h, out))
+        return list(out)
+
+    def sample_dev(self, batch, v, nv, seeds, first_commit, last_row, mask, enc_noise, mlwe_noise, stream=None):
+        """rg_jindo_sample_dev: the randomness Commit draws, on the device (layouts of commit_dev)."""
+        sh = self.params.shapes(batch)
+        sc = seeds.c_struct()
+        check(lib().rg_jindo_sample_dev(self.h, batch, _addr(v, batch * nv * self.params.L), nv, ctypes.byref(sc),
+                                        first_commit, _addr(last_row, _words(sh["last_row"])),
+                                        _addr(mask, _words(sh["mask"])), _addr(enc_noise, _words(sh["enc_noise"])),
+                                        _addr(mlwe_noise, _words(sh["mlwe_noise"])), _stream(stream)))
+
+    def commit_sampled_dev(self, batch, v, nv, seeds, first_commit, incom, enc, mlwe, com, stream=None):
+        """Prover.Commit end to end on the device: sampling + commit (rg_jindo_commit_sampled_dev)."""
+        sh = self.params.shapes(batch)
+        sc = seeds.c_struct()
+        check(lib().rg_jindo_commit_sampled_dev(self.h, batch, _addr(v, batch * nv * self.params.L), nv,
+                                                ctypes.byref(sc), first_commit, _addr(incom, _words(sh["incom"])),
+                                                _addr(enc, _words(sh["enc"])), _addr(mlwe, _words(sh["mlwe_out"])),
+                                                _addr(com, _words(sh["com"])), _stream(stream)))
 
     def commit_core(self, enc, mlwe):
         """The Ajtai core of Commit (prover.go:144-202) from NTT-domain Opening.Encode / MLWE:
@@ -228,6 +289,12 @@ class Prover:
         """Proof.Encode and Proof.MLWE (prover.go:300-314)."""
         check(lib().rg_jindo_eval_respond_dev(self.h, _addr(ob_enc), _addr(ob_mlwe), _addr(chals), _addr(pf_enc),
                                               _addr(pf_mlwe), _stream(stream)))
+
+
+def uniform_words_dev(seed, instance, first_word, n, out, stream=None):
+    """UniformSampler.Sample() words [first_word, first_word + n) of instance `instance` of
+    NewUniformSamplerWithSeed(seed) into the device buffer `out` (rg_uniform_words_dev)."""
+    check(lib().rg_uniform_words_dev(bytes(seed), len(seed), instance, first_word, n, _addr(out, n), _stream(stream)))
 
 
 def NewProver(params, crs):

@@ -104,3 +104,24 @@ def test_ck_stream_stable():
     ck = pyref.commit_key(pyref.JindoParams(q, P["target_n"], P["batch"]), b"Jindo!")
     assert [hashlib.sha256(np.ascontiguousarray(np.array(x, np.uint64)).tobytes()).hexdigest() for x in ck] == G["ck"]
     assert len(h) == 64
+
+
+def test_uniform_sampler_refill_xors_into_buffer():
+    """uniform.go:64-70: every 8192-byte refill is `XORKeyStream(buf, buf)`, so Sample() word
+    w of chunk c = 1024 w-words is KS_0[w] ^ ... ^ KS_c[w] (KS_i = i-th 8192-byte keystream chunk),
+    not plain keystream; the CK derivation (entities.go:21-73) reads ~10^6 words through it."""
+    u = pyref.UniformSampler(b"Jindo!")
+    words = [u.sample() for _ in range(3 * 1024 + 5)]
+    r = hashlib.sha384(b"Jindo!").digest()
+    ks = pyref.aes256_ctr_keystream(r[:32], r[32:48], 4 * 8192)
+    kw = [int.from_bytes(ks[8 * i:8 * i + 8], "little") for i in range(4 * 1024)]
+    for w in (0, 1, 1023):
+        assert words[w] == kw[w]
+    for w in (1024, 1500, 2047):
+        assert words[w] == kw[w] ^ kw[w - 1024]
+    for w in (2048, 3 * 1024 + 4):
+        c, o = divmod(w, 1024)
+        x = 0
+        for i in range(c + 1):
+            x ^= kw[1024 * i + o]
+        assert words[w] == x
