@@ -9,8 +9,9 @@
 // words); an instance rarely reads past its first 1024 words, and when it does the XOR of the
 // earlier chunks is recomputed.
 //
-// AES-256 runs from a T-table held in LDS, replicated 32 times so that lane l always reads
-// bank l & 31 (conflict-free): 32 KiB per workgroup.
+// AES-256 runs from a T-table held in LDS, replicated 64 times so that lane l reads replica l
+// (bank l mod 32, conflict-free) at byte offset (x << 8) | (l << 2), which one v_perm forms from
+// the state word: 64 KiB per workgroup.  Keys come from kernel arguments (SGPRs) or LDS.
 //
 // Samplers (each a literal restatement, floats in IEEE double without contraction):
 //   TwinCDT.Sample        gaussian_twin_cdt.go:77-112 (tables from the host, global memory)
@@ -24,8 +25,10 @@
 
 namespace rg {
 
-constexpr int kAesLds = 256 * 32;  // u32 words of the replicated T-table
-constexpr int kWinShift = 24;      // blocks per sampler instance: 2^24 (256 MiB of keystream)
+constexpr int kAesRep = 64;              // replicas of the T-table: lane l reads replica l
+constexpr int kAesLds = 256 * kAesRep;   // u32 words of the replicated T-table (64 KiB)
+constexpr int kWinShift = 24;            // blocks per sampler instance: 2^24 (256 MiB of keystream)
+constexpr int kKeyWords = 64;            // an AES key staged in LDS: rk[60], iv[4]
 
 struct AesKey {
   uint32_t rk[60];
@@ -37,82 +40,126 @@ struct AesKey {
 
 __device__ __forceinline__ uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-// fill the workgroup's LDS T-table copy (call by all threads, then __syncthreads)
-__device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
-  for (int i = threadIdx.x; i < kAesLds; i += blockDim.x) lds[i] = te0[i >> 5];
+// a ^ b ^ c in one instruction (gfx950 v_bitop3_b32, truth table 0x96); the compiler does not
+// form it from xor chains
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
-__device__ __forceinline__ uint32_t te(const uint32_t* lds, uint32_t x, uint32_t lane) { return lds[(x << 5) | lane]; }
+// fill the workgroup's LDS T-table: word x * 64 + l = Te0[x] (call by all threads, then sync)
+__device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
+  for (int i = threadIdx.x; i < kAesLds; i += blockDim.x) lds[i] = te0[i >> 6];
+}
+// stage one key (round keys + IV) in LDS: kKeyWords words
+__device__ __forceinline__ void aes_key_fill(uint32_t* dst, const AesKey& k) {
+  for (int i = threadIdx.x; i < kKeyWords; i += blockDim.x) dst[i] = i < 60 ? k.rk[i] : k.iv[i - 60];
+}
+
+// Key sources: a key in LDS (per-lane pointer: lanes may use different keys) or a kernel
+// argument whose words the compiler keeps in SGPRs.
+struct LdsKey {
+  const uint32_t* p;
+  __device__ __forceinline__ uint32_t rk(int i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t iv(int i) const { return p[60 + i]; }
+};
+struct ArgKey {
+  const AesKey& k;
+  __device__ __forceinline__ uint32_t rk(int i) const { return k.rk[i]; }
+  __device__ __forceinline__ uint32_t iv(int i) const { return k.iv[i]; }
+};
+
+// T-table lookup of byte `B` of s: the LDS byte offset (byte << 8) | (lane << 2) is one v_perm
+// (byte 1 <- s.byte B, byte 0 <- lane4.byte 0, bytes 2-3 <- 0); bank = lane mod 32, conflict-free
+template <int B>
+__device__ __forceinline__ uint32_t te_b(const uint32_t* lds, uint32_t s, uint32_t lane4) {
+  const uint32_t off = __builtin_amdgcn_perm(s, lane4, 0x0C0C0000u | ((4u + B) << 8));
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + off);
+}
 
 // AES-256 of the counter block IV + n; returns the 16 keystream bytes as 4 big-endian words
-__device__ __forceinline__ void aes_ctr(const AesKey& K, uint64_t n, const uint32_t* lds, uint32_t out[4]) {
-  const uint32_t lane = threadIdx.x & 31u;
-  const uint64_t lo = (((uint64_t)K.iv[2] << 32) | K.iv[3]) + n;
-  const uint64_t hi = (((uint64_t)K.iv[0] << 32) | K.iv[1]) + (lo < n ? 1u : 0u);
-  uint32_t s0 = (uint32_t)(hi >> 32) ^ K.rk[0], s1 = (uint32_t)hi ^ K.rk[1], s2 = (uint32_t)(lo >> 32) ^ K.rk[2],
-           s3 = (uint32_t)lo ^ K.rk[3];
+template <class K>
+__device__ __forceinline__ void aes_ctr(const K& key, uint64_t n, const uint32_t* lds, uint32_t out[4]) {
+  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
+  const uint64_t ivlo = ((uint64_t)key.iv(2) << 32) | key.iv(3), ivhi = ((uint64_t)key.iv(0) << 32) | key.iv(1);
+  const uint64_t lo = ivlo + n;
+  const uint64_t hi = ivhi + (lo < n ? 1u : 0u);
+  uint32_t s0 = (uint32_t)(hi >> 32) ^ key.rk(0), s1 = (uint32_t)hi ^ key.rk(1), s2 = (uint32_t)(lo >> 32) ^ key.rk(2),
+           s3 = (uint32_t)lo ^ key.rk(3);
 #pragma unroll
   for (int r = 1; r < 14; ++r) {
-    const uint32_t t0 = te(lds, s0 >> 24, lane) ^ ror32(te(lds, (s1 >> 16) & 255u, lane), 8) ^
-                        ror32(te(lds, (s2 >> 8) & 255u, lane), 16) ^ ror32(te(lds, s3 & 255u, lane), 24) ^ K.rk[4 * r];
-    const uint32_t t1 = te(lds, s1 >> 24, lane) ^ ror32(te(lds, (s2 >> 16) & 255u, lane), 8) ^
-                        ror32(te(lds, (s3 >> 8) & 255u, lane), 16) ^ ror32(te(lds, s0 & 255u, lane), 24) ^
-                        K.rk[4 * r + 1];
-    const uint32_t t2 = te(lds, s2 >> 24, lane) ^ ror32(te(lds, (s3 >> 16) & 255u, lane), 8) ^
-                        ror32(te(lds, (s0 >> 8) & 255u, lane), 16) ^ ror32(te(lds, s1 & 255u, lane), 24) ^
-                        K.rk[4 * r + 2];
-    const uint32_t t3 = te(lds, s3 >> 24, lane) ^ ror32(te(lds, (s0 >> 16) & 255u, lane), 8) ^
-                        ror32(te(lds, (s1 >> 8) & 255u, lane), 16) ^ ror32(te(lds, s2 & 255u, lane), 24) ^
-                        K.rk[4 * r + 3];
+    const uint32_t t0 = xor3(xor3(te_b<3>(lds, s0, lane4), ror32(te_b<2>(lds, s1, lane4), 8),
+                                  ror32(te_b<1>(lds, s2, lane4), 16)),
+                             ror32(te_b<0>(lds, s3, lane4), 24), key.rk(4 * r));
+    const uint32_t t1 = xor3(xor3(te_b<3>(lds, s1, lane4), ror32(te_b<2>(lds, s2, lane4), 8),
+                                  ror32(te_b<1>(lds, s3, lane4), 16)),
+                             ror32(te_b<0>(lds, s0, lane4), 24), key.rk(4 * r + 1));
+    const uint32_t t2 = xor3(xor3(te_b<3>(lds, s2, lane4), ror32(te_b<2>(lds, s3, lane4), 8),
+                                  ror32(te_b<1>(lds, s0, lane4), 16)),
+                             ror32(te_b<0>(lds, s1, lane4), 24), key.rk(4 * r + 2));
+    const uint32_t t3 = xor3(xor3(te_b<3>(lds, s3, lane4), ror32(te_b<2>(lds, s0, lane4), 8),
+                                  ror32(te_b<1>(lds, s1, lane4), 16)),
+                             ror32(te_b<0>(lds, s2, lane4), 24), key.rk(4 * r + 3));
     s0 = t0;
     s1 = t1;
     s2 = t2;
     s3 = t3;
   }
-  // final round: S-box bytes (byte 2 of Te0[x] is S[x]), no MixColumns
-  auto sb = [&](uint32_t x) { return (te(lds, x, lane) >> 16) & 255u; };
-  out[0] = ((sb(s0 >> 24) << 24) | (sb((s1 >> 16) & 255u) << 16) | (sb((s2 >> 8) & 255u) << 8) | sb(s3 & 255u)) ^ K.rk[56];
-  out[1] = ((sb(s1 >> 24) << 24) | (sb((s2 >> 16) & 255u) << 16) | (sb((s3 >> 8) & 255u) << 8) | sb(s0 & 255u)) ^ K.rk[57];
-  out[2] = ((sb(s2 >> 24) << 24) | (sb((s3 >> 16) & 255u) << 16) | (sb((s0 >> 8) & 255u) << 8) | sb(s1 & 255u)) ^ K.rk[58];
-  out[3] = ((sb(s3 >> 24) << 24) | (sb((s0 >> 16) & 255u) << 16) | (sb((s1 >> 8) & 255u) << 8) | sb(s2 & 255u)) ^ K.rk[59];
+  // final round: S-box bytes (byte 2 of Te0[x] is S[x]) gathered with v_perm, no MixColumns
+  auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    const uint32_t ab = __builtin_amdgcn_perm(te_b<3>(lds, a, lane4), te_b<2>(lds, b, lane4), 0x06020C0Cu);
+    const uint32_t cd = __builtin_amdgcn_perm(te_b<1>(lds, c, lane4), te_b<0>(lds, d, lane4), 0x0C0C0602u);
+    return xor3(ab, cd, k);
+  };
+  out[0] = fin(s0, s1, s2, s3, key.rk(56));
+  out[1] = fin(s1, s2, s3, s0, key.rk(57));
+  out[2] = fin(s2, s3, s0, s1, key.rk(58));
+  out[3] = fin(s3, s0, s1, s2, key.rk(59));
 }
 
 // the two little-endian u64 keystream words of block n
-__device__ __forceinline__ void ks_words(const AesKey& K, uint64_t n, const uint32_t* lds, uint64_t& w0, uint64_t& w1) {
+template <class K>
+__device__ __forceinline__ void ks_words(const K& key, uint64_t n, const uint32_t* lds, uint64_t& w0, uint64_t& w1) {
   uint32_t o[4];
-  aes_ctr(K, n, lds, o);
+  aes_ctr(key, n, lds, o);
   w0 = (uint64_t)bswap32(o[0]) | ((uint64_t)bswap32(o[1]) << 32);
   w1 = (uint64_t)bswap32(o[2]) | ((uint64_t)bswap32(o[3]) << 32);
+}
+__device__ __forceinline__ void ks_words(const AesKey& K, uint64_t n, const uint32_t* lds, uint64_t& w0, uint64_t& w1) {
+  ks_words(ArgKey{K}, n, lds, w0, w1);
+}
+
+// word `p` of the Sample() stream of the instance whose window starts at block `base`
+// (uniform.go:64-82): chunk c = KS_0 ^ ... ^ KS_c
+__device__ __noinline__ uint64_t uniform_word_at(LdsKey key, const uint32_t* lds, uint64_t base, uint64_t p) {
+  const uint64_t c = p >> 10, o = p & 1023u;
+  uint64_t x = 0;
+  for (uint64_t i = 0; i <= c; ++i) {
+    uint64_t w0, w1;
+    ks_words(key, base + ((i << 10) + o) / 2, lds, w0, w1);
+    x ^= (o & 1) ? w1 : w0;
+  }
+  return x;
 }
 
 // One UniformSampler instance (window `inst` of the domain): Sample(), SampleFloat()
 struct Uniform {
-  const AesKey* K;
+  LdsKey key;
   const uint32_t* lds;
   uint64_t base;  // first block of the window
   uint64_t pos;   // next word
   uint64_t spare;
   bool have_spare;
 
-  __device__ __forceinline__ void init(const AesKey& key, const uint32_t* l, uint64_t inst) {
-    K = &key;
+  __device__ __forceinline__ void init(const uint32_t* key_lds, const uint32_t* l, uint64_t inst) {
+    key.p = key_lds;
     lds = l;
     base = inst << kWinShift;
     pos = 0;
     have_spare = false;
   }
-  // word `p` of the instance's Sample() stream (uniform.go:64-82)
-  __device__ uint64_t word_at(uint64_t p) const {
-    const uint64_t c = p >> 10, o = p & 1023u;
-    uint64_t x = 0;
-    for (uint64_t i = 0; i <= c; ++i) {  // chunk c = KS_0 ^ ... ^ KS_c (c = 0 in practice)
-      uint64_t w0, w1;
-      ks_words(*K, base + ((i << 10) + o) / 2, lds, w0, w1);
-      x ^= (o & 1) ? w1 : w0;
-    }
-    return x;
-  }
+  __device__ uint64_t word_at(uint64_t p) const { return uniform_word_at(key, lds, base, p); }
   __device__ __forceinline__ uint64_t sample() {
     uint64_t r;
     if (have_spare) {
@@ -120,7 +167,7 @@ struct Uniform {
       have_spare = false;
     } else if (pos < 1024 && !(pos & 1)) {
       uint64_t w0, w1;
-      ks_words(*K, base + pos / 2, lds, w0, w1);
+      ks_words(key, base + pos / 2, lds, w0, w1);
       r = w0;
       spare = w1;
       have_spare = true;
@@ -150,6 +197,7 @@ __device__ __forceinline__ int64_t cdt_search(const uint64_t* t, int n, uint64_t
 
 struct CdtDev {
   const uint64_t* tables;  // [128][size]
+  const uint8_t* guide;    // [128][257]: lower_bound of t * 2^56 (size <= 255), or null
   int size;
   int64_t tail_lo;
   double sigma;

@@ -1038,6 +1038,25 @@ struct SampleArgs {
   long long* enc_noise;   // [B][cols+1][rows][d]
   long long* mlwe_noise;  // [B][cols+1][nm][d]
   long long n_enc_pairs, n_ml_pairs;
+  long long batch;
+  // TwinCDT v0 != v1 tails deferred by cdt_noise_kernel to cdt_tail_kernel: one segment of
+  // tail_cap entries per wave, entry counts in tail_n
+  struct CdtTail* tails;
+  int* tail_n;
+  long long tail_cap;
+  // COSAC samples left unresolved by a phase of cosac_noise_kernel: a segment per wave
+  unsigned long long* cos_seg;
+  long long cos_cap;
+};
+
+// a TwinCDT sample whose two table searches disagree (twin_cdt.go:95-110): enc_noise[out]
+// holds v1's result; it becomes `alt` (v0's) when u / 2^64 < the exp-sum cdf over x <= v0
+struct CdtTail {
+  unsigned long long out;
+  uint64_t u;
+  double c_frac;
+  long long alt;
+  long long v0;
 };
 
 #pragma clang fp contract(off)
@@ -1060,9 +1079,12 @@ __device__ __forceinline__ double enc_centre(const SampleArgs& a, const uint32_t
 #pragma clang fp contract(on)
 
 // thread = (commit, column, row, coefficient pair): Gaussian samples of one randEncodeTo
-__global__ __launch_bounds__(256) void enc_noise_kernel(SampleArgs a) {
+__global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t keys[2][kKeyWords];
   aes_lds_fill(lds, a.te0);
+  aes_key_fill(keys[0], a.key[kDomCosac]);
+  aes_key_fill(keys[1], a.key[kDomCosacRnd]);
   __syncthreads();
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= a.n_enc_pairs) return;
@@ -1088,17 +1110,694 @@ __global__ __launch_bounds__(256) void enc_noise_kernel(SampleArgs a) {
     for (int h = 0; h < 2; ++h) {
       const int k = 2 * m + h;
       Uniform base, rnd;
-      base.init(a.key[kDomCosac], lds, gpoly * S.d + k);
-      rnd.init(a.key[kDomCosacRnd], lds, gpoly * S.d + k);
+      base.init(keys[0], lds, gpoly * S.d + k);
+      rnd.init(keys[1], lds, gpoly * S.d + k);
       out[k] = cosac(a.zig, base, rnd, enc_centre(a, dg, k), sd);
     }
   }
 }
 
-// thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
-__global__ __launch_bounds__(256) void mlwe_noise_kernel(SampleArgs a) {
+// ---- d = 256 encode noise, split by sampler -----------------------------------------------
+// enc_noise_kernel above runs both samplers in one grid and every sample's slow path inline,
+// so a wave waits for its slowest lane: the TwinCDT exp tail (v0 != v1: ~1/128 of samples, up
+// to |tail_lo| + v0 + 1 exp terms) and COSAC's rejection loop (max over 64 lanes of a ~50%
+// acceptance geometric).  The two kernels below draw the same words from the same instances,
+// so their output is identical:
+//   cdt_noise_kernel    wave per TwinCDT polynomial, 4 coefficients per lane (2 AES blocks);
+//                       the deltaInv centres from 16-byte digit loads; the 128
+//                       tables' high words in LDS (full words from global only on a tie);
+//                       tail samples resolved one at a time by the whole wave (lanes compute
+//                       the exp terms, then the sum in the reference's order via readlane).
+//   cosac_noise_kernel  wave per COSAC polynomial (row 0 and the mask column), the 256 samples
+//                       a queue that lanes refill as they accept (COSAC as a state machine).
+#ifndef RG_VAR
+#define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC)
+#endif
+#pragma clang fp contract(off)
+constexpr int kCdtWaves = 16;       // waves per cdt_noise_kernel workgroup (one workgroup per CU)
+constexpr int kCdtLdsMaxSize = 96;  // tables' high words + guide in LDS when size <= 96 (<= 145 KiB
+                                    // per workgroup with the 64 KiB AES table)
+constexpr int kCdtChunk = 32;       // consecutive polynomials per chunk
+
+__device__ __forceinline__ double rl_f64(double x, int lane) {
+  const uint64_t b = __double_as_longlong(x);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// lower_bound of u in one table: the high words from LDS, the full word from global on a tie;
+// found -> index - 1 (slices.BinarySearch, twin_cdt.go:86-93)
+__device__ __forceinline__ int cdt_search_hi(const uint32_t* hi, const uint64_t* full, int n, uint64_t u) {
+  const uint32_t uh = (uint32_t)(u >> 32);
+  int lo = 0, len = n;
+  while (len > 0) {
+    const int half = len >> 1, mid = lo + half;
+    const uint32_t th = hi[mid];
+    const bool less = th != uh ? th < uh : full[mid] < u;
+    if (less) {
+      lo = mid + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  const bool eq = lo < n && hi[lo] == uh && full[lo] == u;
+  return eq ? lo - 1 : lo;
+}
+
+// lower_bound searches of a lane's 4 samples in tables c0 and c1 (8 searches).  LdsTable: a
+// guide table (per table, the lower_bound of t * 2^56 for t = 0..256, u8) narrows each search
+// to the entries sharing u's top byte, mostly 0-2 of them, then a bisection over that range
+// on the tables' high words in LDS (the full word from global memory only on a tie).
+// Otherwise: plain bisection of the global tables.
+template <bool LdsTable>
+__device__ __forceinline__ void cdt_search8(const uint32_t* thi, const uint8_t* guide, const CdtDev& C, const int tab[8],
+                                            const uint64_t u[4], int res[8]) {
+  const int n = C.size;
+  auto less = [&](int j, int idx) {
+    const uint64_t uj = u[j >> 1];
+    const long long o = (long long)tab[j] * n + idx;
+    if (!LdsTable) return C.tables[o] < uj;
+    const uint32_t th = thi[o], uh = (uint32_t)(uj >> 32);
+    return th != uh ? th < uh : C.tables[o] < uj;  // a tie of the high words: the full word
+  };
+  int lo[8], len[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (LdsTable) {
+      const int t = (int)(u[j >> 1] >> 56);
+      lo[j] = guide[tab[j] * 257 + t];
+      len[j] = guide[tab[j] * 257 + t + 1] - lo[j];  // answer in [lo, lo + len]
+    } else {
+      lo[j] = 0;
+      len[j] = n;
+    }
+  }
+  for (;;) {
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (len[j] > 0) {
+        const int half = len[j] >> 1;
+        if (less(j, lo[j] + half)) {
+          lo[j] += half + 1;
+          len[j] -= half + 1;
+        } else {
+          len[j] = half;
+        }
+        more |= len[j] > 0;
+      }
+    if (!__ballot(more)) break;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = lo[j];  // lower_bound; found -> index - 1 (slices.BinarySearch)
+    const uint64_t uj = u[j >> 1];
+    const long long o = (long long)tab[j] * n + i;
+    bool eq = false;
+    if (i < n) eq = (LdsTable ? thi[o] == (uint32_t)(uj >> 32) : true) && C.tables[o] == uj;
+    res[j] = eq ? i - 1 : i;
+  }
+}
+
+__device__ __forceinline__ double wave_sum_f64(double x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+// dynamic LDS of cdt_noise_kernel<true>: high words [128][size] u32, guide [128][257] u8, key
+__host__ __device__ constexpr int cdt_guide_off(int size) { return 128 * size * 4; }
+__host__ __device__ constexpr int cdt_key_off(int size) { return cdt_guide_off(size) + ((128 * 257 + 3) & ~3); }
+__host__ __device__ constexpr int cdt_dyn_lds(bool lds_table, int size) {
+  return lds_table ? cdt_key_off(size) + kKeyWords * 4 : kKeyWords * 4;
+}
+
+// Each wave owns a contiguous range of the batch's (commit, column, row) polynomials: TwinCDT
+// polynomials are sampled; COSAC ones get their deltaInv centres (as doubles, in enc_noise)
+// for cosac_noise_kernel; skipped ones are zeroed.
+template <bool LdsTable>
+__global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
+  extern __shared__ uint32_t dyn[];
+  const CdtDev& C = a.cdt_enc;
+  uint32_t* thi = dyn;
+  uint8_t* guide = reinterpret_cast<uint8_t*>(dyn) + cdt_guide_off(C.size);
+  uint32_t* keyl = LdsTable ? dyn + cdt_key_off(C.size) / 4 : dyn;
   aes_lds_fill(lds, a.te0);
+  aes_key_fill(keyl, a.key[kDomEncCdt]);
+  if (LdsTable) {
+    for (int i = threadIdx.x; i < 128 * C.size; i += blockDim.x) thi[i] = (uint32_t)(C.tables[i] >> 32);
+    for (int i = threadIdx.x; i < 128 * 257; i += blockDim.x) guide[i] = C.guide[i];
+  }
+  __syncthreads();
+  const JShape& S = a.s;
+  const int lane = threadIdx.x & 63;
+  const long long npoly = a.batch * (S.cols + 1) * S.rows;
+  const long long nw = (long long)gridDim.x * kCdtWaves;
+  const double norm = sqrt(2.0 * M_PI) * C.sigma;
+  const double two_s2 = 2.0 * C.sigma * C.sigma;
+  const LdsKey key{keyl};
+  const long long wv = (long long)blockIdx.x * kCdtWaves + (threadIdx.x >> 6);
+  CdtTail* seg = a.tails + wv * a.tail_cap;
+  long long ntail = 0;
+  // chunks of kCdtChunk consecutive polynomials, dealt round-robin to the waves
+  for (long long p0 = ((long long)blockIdx.x * kCdtWaves + (threadIdx.x >> 6)) * kCdtChunk; p0 < npoly;
+       p0 += nw * kCdtChunk) {
+  const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
+  int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
+  for (long long poly = p0; poly < p1; ++poly) {  // (b, col, row) flattened
+    if (poly > p0 && ++row == S.rows) {
+      row = 0;
+      if (++col == S.cols + 1) col = 0;
+    }
+    long long* out = a.enc_noise + poly * 256;
+    if (enc_skipped(S, col, row)) {  // the reference draws nothing for these (prover.go:101-105,118-123)
+      reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(0, 0);
+      reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(0, 0);
+      continue;
+    }
+    const double sd =
+        col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
+    const bool cdt = sd == a.sd_ecd;
+    const uint32_t* dg = a.digits + poly * 256;
+    // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order)
+    double fp[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < S.exp; ++i) {
+      const double di = a.delta[i];
+      if (di == 0.0) continue;
+      const int base = 4 * lane + (i + 1) * S.slots;  // coefficient k reads digit (k + (i+1) slots) mod 256
+      const uint4 g = *reinterpret_cast<const uint4*>(dg + (base & 255));
+      const uint32_t gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        if (base + h >= 256)
+          fp[h] = fp[h] + di * (double)gv[h];
+        else
+          fp[h] = fp[h] - di * (double)gv[h];
+      }
+    }
+    if (!cdt) {  // a COSAC polynomial: hand the centres to cosac_noise_kernel
+      reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
+      reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
+      continue;
+    }
+    const unsigned long long gpoly =
+        a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
+    uint64_t u[4];
+#if RG_VAR & 2
+    for (int h = 0; h < 4; ++h) u[h] = (gpoly * 0x9E3779B97F4A7C15ull + (uint64_t)(4 * lane + h)) * 0xBF58476D1CE4E5B9ull;
+#else
+    ks_words(key, (gpoly << kWinShift) + (uint64_t)(2 * lane), lds, u[0], u[1]);
+    ks_words(key, (gpoly << kWinShift) + (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
+#endif
+    // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111)
+    int tab[8], v[8];
+    double cf[4], flo[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const double center = -fp[h];
+      flo[h] = floor(center);
+      cf[h] = center - flo[h];
+      tab[2 * h] = (int)((int64_t)floor(128.0 * cf[h]) % 128);
+      tab[2 * h + 1] = (int)((int64_t)ceil(128.0 * cf[h]) % 128);
+    }
+#if RG_VAR & 4
+    for (int j = 0; j < 8; ++j) v[j] = (int)(u[j >> 1] >> 58) + (j & 1);
+#else
+    cdt_search8<LdsTable>(thi, guide, C, tab, u, v);
+#endif
+    int64_t res[4];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      res[h] = (int64_t)v[2 * h + 1] + C.tail_lo + (int64_t)flo[h];
+      if (v[2 * h] != v[2 * h + 1]) pend |= 1u << h;
+    }
+#if RG_VAR & 1
+    pend = 0;
+#endif
+    // the v0 != v1 tails: appended to this wave's segment for cdt_tail_kernel (counts <= 4 per
+    // lane: offsets from three ballots of the count's bits); only if the segment is full are they
+    // resolved here, one at a time across the wave: lanes compute the exp terms, a tree sum
+    // decides p < cdf unless p is within the two sums' error bound of it, and only then the
+    // terms are summed in the reference's order (readlane chain)
+    {
+      const int cnt = __builtin_popcount(pend);
+      const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+      const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+      if (tot && ntail + tot <= a.tail_cap) {
+        auto mb = [](uint64_t m) {
+          return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        };
+        long long o = ntail + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if (pend & (1u << h)) {
+            CdtTail t;
+            t.out = (unsigned long long)(poly * 256 + 4 * lane + h);
+            t.u = u[h];
+            t.c_frac = cf[h];
+            t.alt = (int64_t)v[2 * h] + C.tail_lo + (int64_t)flo[h];
+            t.v0 = v[2 * h];
+            seg[o++] = t;
+          }
+        ntail += tot;
+        pend = 0;
+      }
+    }
+    for (;;) {
+      const uint64_t any = __ballot(pend != 0);
+      if (!any) break;
+      const int src = __builtin_amdgcn_readfirstlane(__builtin_ctzll(any));
+      const int hs = __builtin_amdgcn_readlane(pend ? __builtin_ctz(pend) : 0, src);
+      double c_frac = 0.0, p = 0.0;
+      int v0 = 0;
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+        if (h == hs) {
+          c_frac = cf[h];
+          v0 = v[2 * h];
+          p = __ull2double_rn(u[h]) / 18446744073709551616.0;
+        }
+      c_frac = rl_f64(c_frac, src);
+      v0 = __builtin_amdgcn_readlane(v0, src);
+      const int nterm = (int)((int64_t)v0 - C.tail_lo + 1);
+      double approx = 0.0;
+      for (int64_t x0 = C.tail_lo; x0 <= v0; x0 += 64) {
+        const double xf = (double)(x0 + lane);
+        const double term = x0 + lane <= v0 ? exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm : 0.0;
+        approx += wave_sum_f64(term);
+      }
+      // |tree sum - sequential sum| <= 2 (n-1) 2^-53 sum (+ a margin)
+      const double bound = approx * (4.0 * (nterm + 2)) * 1.1102230246251565e-16;
+      bool lt = p < approx;
+      const bool close = fabs(p - approx) <= bound;
+      if (__builtin_amdgcn_readlane((int)close, src)) {
+        double cdf = 0.0;
+        for (int64_t x0 = C.tail_lo; x0 <= v0; x0 += 64) {
+          const double xf = (double)(x0 + lane);
+          const double term = exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm;
+          const int nn = (int)std::min<int64_t>(64, (int64_t)v0 - x0 + 1);
+          for (int i = 0; i < nn; ++i) cdf += rl_f64(term, i);
+        }
+        lt = p < cdf;
+      }
+      if (lane == src) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if (h == hs && lt) res[h] = (int64_t)v[2 * h] + C.tail_lo + (int64_t)flo[h];
+        pend &= pend - 1;
+      }
+    }
+    reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(res[0], res[1]);
+    reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(res[2], res[3]);
+  }
+  }
+  if (lane == 0) a.tail_n[wv] = (int)ntail;
+}
+
+// The deferred TwinCDT tails: wave w resolves segment w, two entries at a time (32 lanes each):
+// each lane sums its share of the exp terms, a 32-lane tree sum decides p < cdf unless p lies
+// within the error bound of both sums, then the terms are summed in the reference's order.
+__global__ __launch_bounds__(256) void cdt_tail_kernel(SampleArgs a) {
+  const CdtDev& C = a.cdt_enc;
+  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int n = a.tail_n[wv];
+  const CdtTail* seg = a.tails + wv * a.tail_cap;
+  const double norm = sqrt(2.0 * M_PI) * C.sigma;
+  const double two_s2 = 2.0 * C.sigma * C.sigma;
+  for (int e0 = 0; e0 < n; e0 += 2) {
+    const int e = e0 + half < n ? e0 + half : e0;
+    const CdtTail t = seg[e];
+    double part = 0.0;
+    for (long long x = C.tail_lo + hl; x <= t.v0; x += 32) {
+      const double xf = (double)x;
+      part += exp(-(xf - t.c_frac) * (xf - t.c_frac) / two_s2) / norm;
+    }
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) part += __shfl_xor(part, m, 64);
+    const double p = __ull2double_rn(t.u) / 18446744073709551616.0;
+    const int nterm = (int)(t.v0 - C.tail_lo + 1);
+    const double bound = part * (4.0 * (nterm + 2)) * 1.1102230246251565e-16;
+    bool lt = p < part;
+    const bool close = fabs(p - part) <= bound;
+    for (int hh = 0; hh < 2; ++hh) {  // exact sums (rare), one entry at a time across the wave
+      if (!__builtin_amdgcn_readlane((int)close, 32 * hh)) continue;
+      const double c_frac = rl_f64(t.c_frac, 32 * hh);
+      const long long v0 = (long long)__builtin_amdgcn_readlane((int)t.v0, 32 * hh);
+      double cdf = 0.0;
+      for (long long x0 = C.tail_lo; x0 <= v0; x0 += 64) {
+        const double xf = (double)(x0 + lane);
+        const double term = exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm;
+        const int nn = (int)std::min<long long>(64, v0 - x0 + 1);
+        for (int i = 0; i < nn; ++i) cdf += rl_f64(term, i);
+      }
+      if (half == hh) lt = p < cdf;
+    }
+    if (hl == 0 && e0 + half < n && lt) a.enc_noise[t.out] = t.alt;
+  }
+}
+
+// COSACSampler.Sample (gaussian_cosac.go:22-57) with its RoundedGaussianSampler's normFloat
+// (gaussian_rounded.go:77-116) as a state machine in which every state consumes exactly one
+// Sample() word, from the sampler's own instance (base) or the rounded sampler's (rnd):
+enum { kCoStart = 0, kCoNorm, kCoTailU, kCoTailV, kCoWedge, kCoBit, kCoRR };
+__device__ __forceinline__ int co_src(int st) { return (st >= kCoNorm && st <= kCoWedge) ? 1 : 0; }
+
+struct CosacLane {
+  long long g;     // queue index of the current sample, -1: none
+  long long* out;  // its output word
+  unsigned long long inst;
+  int st, zi;
+  uint64_t pos[2], spare[2];
+  bool have[2];
+  uint64_t zb;
+  double sd, two_s2, lead, inv_lead, c_int, c_frac, x, u, y, y_round;
+};
+
+__device__ __forceinline__ double float52(uint64_t w) { return (double)(w & 0xFFFFFFFFFFFFFull) * 2.220446049250313e-16; }
+
+__device__ __forceinline__ void cosac_step(CosacLane& L, uint64_t w, const ZigDev& Z) {
+  const double rn = 3.442619855899;
+  const int st = L.st;
+  const double fw = float52(w);
+  // the one exp / log a state may need, evaluated once for all lanes that need it.  The exp is
+  // skipped where its comparison is decided without it: START rejects when r >= 1 / lead
+  // (exp <= 1, and / is monotone); RR accepts when arg >= 0 (exp >= 1 > rr) or when
+  // rr < (1 + arg)(1 - 2^-48) <= exp(arg) (exp(a) >= 1 + a; exp within an ulp)
+  double arg = 0.0;
+  bool need_e = false, acc = false;
+  if (st == kCoStart) {
+    arg = -(L.c_frac * L.c_frac) / L.two_s2;
+    need_e = fw < L.inv_lead;
+  }
+  if (st == kCoWedge) {
+    arg = -0.5 * L.x * L.x;
+    need_e = true;
+  }
+  if (st == kCoRR) {
+    arg = -((L.y_round + L.c_frac) * (L.y_round + L.c_frac) - L.y * L.y) / L.two_s2;
+    acc = arg >= 0.0 || fw < (1.0 + arg) * 0.99999999999999644729;
+    need_e = !acc;
+  }
+  double e = 0.0, lg = 0.0;
+  if (need_e) e = exp(arg);
+  if (st == kCoTailU || st == kCoTailV) lg = -log(fw);
+  double nf = 0.0;
+  bool have_nf = false;
+  switch (st) {
+    case kCoStart:  // gaussian_cosac.go:36-40
+      if (need_e && fw < e / L.lead) {
+        *L.out = (int64_t)L.c_int;
+        L.g = -1;
+      } else {
+        L.st = kCoNorm;
+      }
+      break;
+    case kCoNorm: {  // gaussian_rounded.go:80-92
+      const uint64_t b = w >> 63;
+      const uint32_t i = (uint32_t)(w & 127u);
+      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
+      const double x = (double)(int64_t)((j ^ (0ull - b)) + b) * Z.wn[i];
+      if (j < Z.kn[i]) {
+        nf = x;
+        have_nf = true;
+      } else if (i == 0) {
+        L.zb = b;
+        L.st = kCoTailU;
+      } else {
+        L.zi = (int)i;
+        L.x = x;
+        L.st = kCoWedge;
+      }
+      break;
+    }
+    case kCoTailU:  // gaussian_rounded.go:94-101
+      L.u = lg * (1.0 / rn);
+      L.st = kCoTailV;
+      break;
+    case kCoTailV:
+      if (lg + lg >= L.u * L.u) {
+        const double uu = L.u + rn;
+        nf = L.zb == 1 ? -uu : uu;
+        have_nf = true;
+      } else {
+        L.st = kCoTailU;
+      }
+      break;
+    case kCoWedge: {  // gaussian_rounded.go:109-113
+      const double f0 = Z.fn[L.zi - 1], f1 = Z.fn[L.zi];
+      if (fw * (f0 - f1) < e - f1) {
+        nf = L.x;
+        have_nf = true;
+      } else {
+        L.st = kCoNorm;
+      }
+      break;
+    }
+    case kCoBit: {  // gaussian_cosac.go:43-50
+      bool cmp;
+      if ((w & 1) == 0) {
+        L.y_round = round(L.y) - 1.0;
+        cmp = L.y_round <= 0.5;
+      } else {
+        L.y_round = round(L.y) + 1.0;
+        cmp = L.y_round >= -0.5;
+      }
+      L.st = cmp ? kCoRR : kCoNorm;
+      break;
+    }
+    default:  // kCoRR, gaussian_cosac.go:51-55
+      if (acc || fw < e) {
+        *L.out = (int64_t)L.y_round + (int64_t)L.c_int;
+        L.g = -1;
+      } else {
+        L.st = kCoNorm;
+      }
+      break;
+  }
+  if (have_nf) {
+    L.y = L.sd * nf;
+    L.st = kCoBit;
+  }
+}
+
+// COSAC with its words precomputed: KB blocks (2 KB words) of the sampler's own instance and
+// KR blocks of the rounded sampler's, all lanes in lockstep, then the reference's control flow
+// (gaussian_cosac.go:22-57, normFloat's fast path gaussian_rounded.go:80-92) from registers
+// for up to 2 KR rejection-loop passes.  Returns false (nothing written) when the sample needs
+// more: a ziggurat wedge/tail draw, more passes or more words; the caller restarts it with
+// more blocks or in the state machine.  Exp shortcuts as in cosac_step.
+template <int KB, int KR>
+__device__ __forceinline__ bool cosac_fast(const LdsKey& kb, const LdsKey& kr, const uint32_t* lds,
+                                           unsigned long long inst, double center, double sd, const ZigDev& Z,
+                                           long long& res) {
+  uint64_t bw[2 * KB], rw[2 * KR];
+  const uint64_t w0 = inst << kWinShift;
+#pragma unroll
+  for (int i = 0; i < KB; ++i) ks_words(kb, w0 + i, lds, bw[2 * i], bw[2 * i + 1]);
+#pragma unroll
+  for (int i = 0; i < KR; ++i) ks_words(kr, w0 + i, lds, rw[2 * i], rw[2 * i + 1]);
+  const double two_s2 = 2.0 * sd * sd;
+  const double lead = sqrt(2.0 * M_PI) * sd;
+  const double c_int = round(center);
+  const double c_frac = c_int - center;
+  const double r = float52(bw[0]);
+  if (r < 1.0 / lead && r < exp(-(c_frac * c_frac) / two_s2) / lead) {
+    res = (long long)c_int;
+    return true;
+  }
+  int bp = 1;
+  bool done = false, fail = false;
+#pragma unroll
+  for (int it = 0; it < 2 * KR; ++it) {
+    if (!done && !fail) {
+      const uint64_t w = rw[it];
+      const uint64_t sb = w >> 63;
+      const uint32_t i = (uint32_t)(w & 127u);
+      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
+      if (!(j < Z.kn[i])) {
+        fail = true;  // normFloat's wedge / tail: more rounded-sampler words
+      } else {
+        const double y = sd * ((double)(int64_t)((j ^ (0ull - sb)) + sb) * Z.wn[i]);
+        uint64_t wb = 0;
+#pragma unroll
+        for (int q = 1; q < 2 * KB; ++q)
+          if (q == bp) wb = bw[q];
+        if (bp >= 2 * KB) fail = true;
+        ++bp;
+        double y_round;
+        bool cmp;
+        if ((wb & 1) == 0) {
+          y_round = round(y) - 1.0;
+          cmp = y_round <= 0.5;
+        } else {
+          y_round = round(y) + 1.0;
+          cmp = y_round >= -0.5;
+        }
+        if (!fail && cmp) {
+          uint64_t wr = 0;
+#pragma unroll
+          for (int q = 1; q < 2 * KB; ++q)
+            if (q == bp) wr = bw[q];
+          if (bp >= 2 * KB) fail = true;
+          ++bp;
+          if (!fail) {
+            const double rr = float52(wr);
+            const double arg = -((y_round + c_frac) * (y_round + c_frac) - y * y) / two_s2;
+            if (arg >= 0.0 || rr < (1.0 + arg) * 0.99999999999999644729 || rr < exp(arg)) {
+              res = (long long)y_round + (long long)c_int;
+              done = true;
+            }
+          }
+        }
+      }
+    }
+  }
+  return done;
+}
+
+// COSAC polynomials: row 0 of the data columns (ecdBlindStdDev) and the mask column
+// (maskBlindStdDev, maskStdDev); job j of a commit is (j, 0) for j < cols, else
+// (cols, j - cols).  Each wave owns jobs wid, wid + nwaves, ... and works in three phases:
+//   1. every sample: cosac_fast<2, 1> (3 blocks; resolves ~3/4: <= 2 loop passes);
+//   2. the rest, restarted: cosac_fast<3, 2> (5 blocks; <= 4 passes);
+//   3. the rest (~1/16), restarted in the state machine below: a queue that lanes refill as
+//      they accept; per iteration every lane first consumes its buffered words, then ONE AES
+//      block is computed for all lanes that need a new one.
+// Unresolved samples go to the wave's segment of a.cos_seg as enc_noise index | sd code << 62
+// (phase 2 compacts it in place).  The deltaInv centres were written into enc_noise by
+// cdt_noise_kernel; instance = polys_before * 256 + enc_noise index.
+constexpr int kCosacThreads = 512;
+__global__ __launch_bounds__(kCosacThreads) void cosac_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t keys[2][kKeyWords];
+  __shared__ uint64_t zig[384];  // kn, wn, fn
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(keys[0], a.key[kDomCosac]);
+  aes_key_fill(keys[1], a.key[kDomCosacRnd]);
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    zig[i] = a.zig.kn[i];
+    zig[128 + i] = __double_as_longlong(a.zig.wn[i]);
+    zig[256 + i] = __double_as_longlong(a.zig.fn[i]);
+  }
+  __syncthreads();
+  const ZigDev Z{zig, reinterpret_cast<const double*>(zig + 128), reinterpret_cast<const double*>(zig + 256)};
+  const LdsKey kb{keys[0]}, kr{keys[1]};
+  const JShape& S = a.s;
+  const int lane = threadIdx.x & 63;
+  const long long nwaves = (long long)gridDim.x * (kCosacThreads / 64);
+  const long long wid = (long long)blockIdx.x * (kCosacThreads / 64) + (threadIdx.x >> 6);
+  const int per = S.cols + S.rows;
+  const long long njobs = a.batch * per;
+  const unsigned long long pb256 = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * 256ull;
+  const double sds[3] = {a.sd_ecd_blind, a.sd_mask, a.sd_mask_blind};
+  unsigned long long* seg = a.cos_seg + wid * a.cos_cap;
+  auto mb = [](uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  };
+  // ---- phase 1 ----
+  long long nseg = 0;
+  for (long long job = wid; job < njobs; job += nwaves) {
+    const long long b = job / per;
+    const int j = (int)(job % per);
+    const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
+    const int code = col < S.cols ? 0 : (row == 0 ? 2 : 1);
+    const double sd = sds[code];
+    if (enc_skipped(S, col, row) || sd == a.sd_ecd) continue;
+    const long long poly = (b * (S.cols + 1) + col) * S.rows + row;
+    for (int k = lane; k < 256; k += 64) {
+      const unsigned long long oi = (unsigned long long)(poly * 256 + k);
+      long long res = 0;
+      const bool ok = cosac_fast<2, 1>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sd, Z, res);
+      if (ok) a.enc_noise[oi] = res;
+      const uint64_t fm = __ballot(!ok);
+      if (!ok) seg[nseg + mb(fm)] = oi | ((unsigned long long)code << 62);
+      nseg += __builtin_popcountll(fm);
+    }
+  }
+  // ---- phase 2 (in-place compaction: entry i is read before any write at index <= i) ----
+  long long n2 = 0;
+  for (long long i0 = 0; i0 < nseg; i0 += 64) {
+    const bool act = i0 + lane < nseg;
+    const unsigned long long ent = act ? seg[i0 + lane] : 0;
+    const unsigned long long oi = ent & ((1ull << 62) - 1);
+    bool ok = true;
+    if (act) {
+      long long res = 0;
+      ok = cosac_fast<3, 2>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sds[ent >> 62], Z, res);
+      if (ok) a.enc_noise[oi] = res;
+    }
+    const uint64_t fm = __ballot(!ok);
+    if (!ok) seg[n2 + mb(fm)] = ent;
+    n2 += __builtin_popcountll(fm);
+  }
+  // ---- phase 3: the state machine over the n2 remaining samples ----
+  CosacLane L;
+  L.g = -1;
+  L.st = 0;
+  long long next = 0;
+  for (;;) {
+    const uint64_t need = __ballot(L.g < 0);
+    const int rank = mb(need);
+    if (L.g < 0 && next + rank < n2) {  // take the next sample of the queue
+      L.g = next + rank;
+      const unsigned long long ent = seg[L.g];
+      const unsigned long long oi = ent & ((1ull << 62) - 1);
+      L.sd = sds[ent >> 62];
+      L.out = a.enc_noise + oi;
+      const double center = __longlong_as_double(*L.out);
+      L.inst = pb256 + oi;
+      L.two_s2 = 2.0 * L.sd * L.sd;
+      L.lead = sqrt(2.0 * M_PI) * L.sd;
+      L.inv_lead = 1.0 / L.lead;
+      L.c_int = round(center);
+      L.c_frac = L.c_int - center;
+      L.st = kCoStart;
+      L.pos[0] = L.pos[1] = 0;
+      L.have[0] = L.have[1] = false;
+    }
+    next += __builtin_popcountll(need);
+    if (!__ballot(L.g >= 0)) break;
+    // 1. buffered words (the second word of the instance's last block)
+    for (;;) {
+      const int s = co_src(L.st);
+      const bool can = L.g >= 0 && L.have[s];
+      if (!__ballot(can)) break;
+      if (can) {
+        L.have[s] = false;
+        ++L.pos[s];
+        cosac_step(L, L.spare[s], Z);
+      }
+    }
+    // 2. one keystream block for every lane whose next word starts a new block
+    if (L.g >= 0) {
+      const int s = co_src(L.st);
+      const uint64_t p = L.pos[s];
+      uint64_t w0, w1;
+      if (p < 1024) {
+        ks_words(LdsKey{keys[s]}, (L.inst << kWinShift) + p / 2, lds, w0, w1);
+        L.spare[s] = w1;
+        L.have[s] = true;
+      } else {  // past the first 8 KiB buffer: the XOR-accumulated refill (rare)
+        w0 = uniform_word_at(LdsKey{keys[s]}, lds, L.inst << kWinShift, p);
+      }
+      ++L.pos[s];
+      cosac_step(L, w0, Z);
+    }
+  }
+}
+#pragma clang fp contract(on)
+
+// thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
+__global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t key[kKeyWords];
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(key, a.key[kDomMlweRnd]);
   __syncthreads();
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= a.n_ml_pairs) return;
@@ -1118,7 +1817,7 @@ __global__ __launch_bounds__(256) void mlwe_noise_kernel(SampleArgs a) {
     for (int h = 0; h < 2; ++h) {
       const int k = 2 * m + h;
       Uniform u;
-      u.init(a.key[kDomMlweRnd], lds, gpoly * S.d + k);
+      u.init(key, lds, gpoly * S.d + k);
       out[k] = rounded_gauss(a.zig, u, 0.0, a.sd_mask_mlwe);
     }
   }
@@ -1143,9 +1842,11 @@ struct UniArgs {
 };
 
 template <int L>
-__global__ __launch_bounds__(256) void uniform_elems_kernel(UniArgs<L> a) {
+__global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
   __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t key[kKeyWords];
   aes_lds_fill(lds, a.te0);
+  aes_key_fill(key, a.key);
   __syncthreads();
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= a.total) return;
@@ -1159,7 +1860,7 @@ __global__ __launch_bounds__(256) void uniform_elems_kernel(UniArgs<L> a) {
     return;
   }
   Uniform u;
-  u.init(a.key, lds, (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i);
+  u.init(key, lds, (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i);
   uint64_t word = 0;
   int left = 0;  // unread bytes of `word`
   for (;;) {
@@ -1188,15 +1889,17 @@ __global__ __launch_bounds__(256) void uniform_elems_kernel(UniArgs<L> a) {
 }
 
 // raw Sample() words of one UniformSampler instance (rg_uniform_words_dev)
-__global__ __launch_bounds__(256) void uniform_words_kernel(AesKey key, const uint32_t* te0, unsigned long long inst,
+__global__ __launch_bounds__(512) void uniform_words_kernel(AesKey key, const uint32_t* te0, unsigned long long inst,
                                                             unsigned long long first, long long n, uint64_t* out) {
   __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t kl[kKeyWords];
   aes_lds_fill(lds, te0);
+  aes_key_fill(kl, key);
   __syncthreads();
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n) return;
   Uniform u;
-  u.init(key, lds, inst);
+  u.init(kl, lds, inst);
   out[gid] = u.word_at(first + (unsigned long long)gid);
 }
 }  // namespace rg
@@ -1210,6 +1913,8 @@ __global__ __launch_bounds__(256) void uniform_words_kernel(AesKey key, const ui
 struct rg_jindo_scratch {
   rg::DevBuf digits, com, ocom;
   rg::DevBuf last, mask, en, mn;  // the sampled randomness of rg_jindo_commit_sampled_dev
+  rg::DevBuf tails, tail_n;       // deferred TwinCDT tails (cdt_noise_kernel -> cdt_tail_kernel)
+  rg::DevBuf cos_seg;             // COSAC samples carried between the phases of cosac_noise_kernel
 };
 
 // Sampler setup (rg_jindo_set_stddevs): the reference's six standard deviations and the tables
@@ -1217,7 +1922,7 @@ struct rg_jindo_scratch {
 struct rg_jindo_samplers {
   bool ready = false;
   double sd[6];  // ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe
-  rg::DevBuf te0, cdt_enc, cdt_mlwe, zig, delta;
+  rg::DevBuf te0, cdt_enc, cdt_guide, cdt_mlwe, zig, delta;
   int cdt_enc_size = 0, cdt_mlwe_size = 0;
   int64_t tail_lo_enc = 0, tail_lo_mlwe = 0;
   std::vector<double> h_delta;
@@ -1735,14 +2440,14 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.last_row = last;
   a.mask = mask;
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
-  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)((a.total + 255) / 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)((a.total + 511) / 512)), dim3(512), 0, st, a);
   return check_launch("jindo uniform");
 }
 
 // lastRow/mask (crypto/rand), then digits, then every Gaussian sample of the batch
 static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const rg_jindo_seeds* seeds,
                               unsigned long long first, uint64_t* d_last, uint64_t* d_mask, int64_t* d_en,
-                              int64_t* d_mn, uint32_t* digits, hipStream_t st) {
+                              int64_t* d_mn, uint32_t* digits, rg_jindo_scratch* sc, hipStream_t st) {
   const rg_jindo_params& p = J->p;
   if (!J->smp.ready) {
     set_last_error("rg_jindo_set_stddevs was not called on this handle");
@@ -1767,8 +2472,8 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   a.first_commit = first;
   a.digits = digits;
   a.delta = S.delta.as<double>();
-  a.cdt_enc = CdtDev{S.cdt_enc.as<uint64_t>(), S.cdt_enc_size, S.tail_lo_enc, S.sd[0]};
-  a.cdt_mlwe = CdtDev{S.cdt_mlwe.as<uint64_t>(), S.cdt_mlwe_size, S.tail_lo_mlwe, S.sd[4]};
+  a.cdt_enc = CdtDev{S.cdt_enc.as<uint64_t>(), S.cdt_guide.as<uint8_t>(), S.cdt_enc_size, S.tail_lo_enc, S.sd[0]};
+  a.cdt_mlwe = CdtDev{S.cdt_mlwe.as<uint64_t>(), nullptr, S.cdt_mlwe_size, S.tail_lo_mlwe, S.sd[4]};
   const uint64_t* zg = S.zig.as<uint64_t>();
   a.zig = ZigDev{zg, reinterpret_cast<const double*>(zg + 128), reinterpret_cast<const double*>(zg + 256)};
   a.sd_ecd = S.sd[0];
@@ -1781,9 +2486,48 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   const int nm = p.in_msis + p.mlwe;
   a.n_enc_pairs = (long long)batch * (p.cols + 1) * p.rows * (p.d / 2);
   a.n_ml_pairs = (long long)batch * (p.cols + 1) * nm * (p.d / 2);
-  hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 255) / 256)), dim3(256), 0, st, a);
-  RG_TRY(check_launch("jindo enc noise"));
-  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)((a.n_ml_pairs + 255) / 256)), dim3(256), 0, st, a);
+  a.batch = (long long)batch;
+  if (p.d == 256) {
+    const long long npoly = (long long)batch * (p.cols + 1) * p.rows;
+    const unsigned g = (unsigned)std::min<long long>((npoly + kCdtWaves - 1) / kCdtWaves, 256);
+    // tail segments: 1/64 of a wave's samples (TwinCDT tails run near 1/128) + 256
+    const long long nw = (long long)g * kCdtWaves;
+    const long long chunks = (npoly + kCdtChunk - 1) / kCdtChunk;
+    a.tail_cap = (chunks + nw - 1) / nw * kCdtChunk * 256 / 64 + 256;
+    {
+      std::lock_guard<std::mutex> lk(J->mu);
+      const size_t tb = (size_t)(nw * a.tail_cap) * sizeof(CdtTail), nb = (size_t)nw * sizeof(int);
+      if (sc->tails.bytes < tb || sc->tail_n.bytes < nb) RG_HIP(hipStreamSynchronize(st));
+      RG_TRY(sc->tails.alloc(tb));
+      RG_TRY(sc->tail_n.alloc(nb));
+    }
+    a.tails = sc->tails.as<CdtTail>();
+    a.tail_n = sc->tail_n.as<int>();
+    if (S.cdt_enc_size <= kCdtLdsMaxSize)
+      hipLaunchKernelGGL(cdt_noise_kernel<true>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(true, S.cdt_enc_size), st, a);
+    else
+      hipLaunchKernelGGL(cdt_noise_kernel<false>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(false, 0), st, a);
+    RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
+    hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)(nw / 4)), dim3(256), 0, st, a);
+    RG_TRY(check_launch("jindo enc noise (TwinCDT tails)"));
+    const long long ncos = (long long)batch * (p.cols + p.rows);  // jobs
+    const long long wpb = kCosacThreads / 64;
+    const unsigned gc = (unsigned)std::min<long long>((ncos + wpb - 1) / wpb, 1024);
+    a.cos_cap = (ncos + (long long)gc * wpb - 1) / ((long long)gc * wpb) * 256;  // every sample of its jobs
+    {
+      std::lock_guard<std::mutex> lk(J->mu);
+      const size_t cb = (size_t)gc * wpb * a.cos_cap * 8;
+      if (sc->cos_seg.bytes < cb) RG_HIP(hipStreamSynchronize(st));
+      RG_TRY(sc->cos_seg.alloc(cb));
+    }
+    a.cos_seg = sc->cos_seg.as<unsigned long long>();
+    hipLaunchKernelGGL(cosac_noise_kernel, dim3(gc), dim3(kCosacThreads), 0, st, a);
+    RG_TRY(check_launch("jindo enc noise (COSAC)"));
+  } else {
+    hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 511) / 512)), dim3(512), 0, st, a);
+    RG_TRY(check_launch("jindo enc noise"));
+  }
+  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)((a.n_ml_pairs + 511) / 512)), dim3(512), 0, st, a);
   return check_launch("jindo mlwe noise");
 }
 
@@ -2140,6 +2884,21 @@ rg_status rg_jindo_set_stddevs(rg_jindo* J, const rg_jindo_stddevs* sd) {
   S.tail_lo_enc = -(int64_t)std::ceil(9.0 * v[0]);
   S.tail_lo_mlwe = -(int64_t)std::ceil(9.0 * v[4]);
   RG_TRY(S.cdt_enc.upload(enc.data(), enc.size() * 8));
+  if (S.cdt_enc_size <= 255) {  // guide: per table, lower_bound of t * 2^56 for t = 0..256
+    std::vector<uint8_t> guide(128 * 257);
+    for (int c = 0; c < 128; ++c) {
+      const uint64_t* t = enc.data() + (size_t)c * S.cdt_enc_size;
+      for (int b = 0; b <= 256; ++b) {
+        int i = 0;
+        if (b == 256)
+          i = S.cdt_enc_size;
+        else
+          while (i < S.cdt_enc_size && t[i] < ((uint64_t)b << 56)) ++i;
+        guide[c * 257 + b] = (uint8_t)i;
+      }
+    }
+    RG_TRY(S.cdt_guide.upload(guide.data(), guide.size()));
+  }
   RG_TRY(S.cdt_mlwe.upload(ml.data(), ml.size() * 8));
   const Ziggurat Z = make_ziggurat();
   std::vector<uint64_t> zg(384);
@@ -2173,7 +2932,7 @@ rg_status rg_jindo_sample_dev(const rg_jindo* J, size_t batch, const uint64_t* d
   rg_jindo_scratch* sc = nullptr;
   RG_TRY(stream_scratch(Jm, batch, st, &sc));
   return sample_stage(Jm, batch, d_v, nv, seeds, first_commit, d_last_row, d_mask, d_enc_noise, d_mlwe_noise,
-                      sc->digits.as<uint32_t>(), st);
+                      sc->digits.as<uint32_t>(), sc, st);
 }
 
 rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv,
@@ -2191,7 +2950,7 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   RG_TRY(sample_scratch(Jm, batch, sc, st));
   uint32_t* digits = sc->digits.as<uint32_t>();
   RG_TRY(sample_stage(Jm, batch, d_v, nv, seeds, first_commit, sc->last.as<uint64_t>(), sc->mask.as<uint64_t>(),
-                      sc->en.as<int64_t>(), sc->mn.as<int64_t>(), digits, st));
+                      sc->en.as<int64_t>(), sc->mn.as<int64_t>(), digits, sc, st));
   return commit_from_digits(Jm, batch, nv, digits, sc->en.as<int64_t>(), sc->mn.as<int64_t>(), d_incom, d_enc, d_mlwe,
                             d_com, sc, st);
 }
@@ -2215,7 +2974,7 @@ rg_status rg_uniform_words_dev(const uint8_t* seed, size_t seed_len, unsigned lo
   DevBuf t;
   RG_TRY(t.upload(te0, sizeof(te0)));
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(uniform_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, t.as<uint32_t>(),
+  hipLaunchKernelGGL(uniform_words_kernel, dim3((unsigned)((n + 511) / 512)), dim3(512), 0, st, K, t.as<uint32_t>(),
                      instance, first_word, (long long)n, d_out);
   RG_TRY(check_launch("uniform words"));
   RG_HIP(hipStreamSynchronize(st));  // `t` is freed on return

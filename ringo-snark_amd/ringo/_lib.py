@@ -5,7 +5,7 @@ import os
 import re
 
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_ROOT, "lib", "libringo.so")
+LIB_PATH = os.environ.get("RINGO_LIB") or os.path.join(_ROOT, "lib", "libringo.so")  # RINGO_LIB: profiling variants
 HEADER = os.path.join(os.path.dirname(_ROOT), "include", "ringo.h")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)

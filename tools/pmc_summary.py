@@ -6,12 +6,12 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 acc = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 dur = defaultdict(list)
-for f in sorted(glob.glob(f"{root}/p*/run_kernel_trace.csv")):
+for f in sorted(glob.glob(f"{root}/p*/**/*kernel_trace.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 for name, cs in acc.items():
