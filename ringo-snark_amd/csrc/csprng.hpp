@@ -9,9 +9,10 @@
 // words); an instance rarely reads past its first 1024 words, and when it does the XOR of the
 // earlier chunks is recomputed.
 //
-// AES-256 runs from a T-table held in LDS, replicated 64 times so that lane l reads replica l
-// (bank l mod 32, conflict-free) at byte offset (x << 8) | (l << 2), which one v_perm forms from
-// the state word: 64 KiB per workgroup.  Keys come from kernel arguments (SGPRs) or LDS.
+// AES-256 runs from T-tables Te0 and Te1 = ror8 Te0 held in LDS, replicated 32 times so that lane
+// l reads replica l % 32 (conflict-free) at byte offset (x << 8) | (Te1 ? 0x80 : 0) | ((l % 32) << 2),
+// which one v_perm forms from the state word: 64 KiB per workgroup.
+// Keys come from kernel arguments (SGPRs) or LDS.
 //
 // Samplers (each a literal restatement, floats in IEEE double without contraction):
 //   TwinCDT.Sample        gaussian_twin_cdt.go:77-112 (tables from the host, global memory)
@@ -25,10 +26,10 @@
 
 namespace rg {
 
-constexpr int kAesRep = 64;              // replicas of the T-table: lane l reads replica l
-constexpr int kAesLds = 256 * kAesRep;   // u32 words of the replicated T-table (64 KiB)
+constexpr int kAesRep = 32;              // replicas of Te0 and Te1: lane l reads replica l % 32
+constexpr int kAesLds = 256 * kAesRep * 2;  // u32 words: per x, 32 x Te0[x] then 32 x Te1[x] (64 KiB)
 constexpr int kWinShift = 24;            // blocks per sampler instance: 2^24 (256 MiB of keystream)
-constexpr int kKeyWords = 64;            // an AES key staged in LDS: rk[60], iv[4]
+constexpr int kKeyWords = 128;           // an AES key staged in LDS: rk[60], iv[4], rol16(rk)[60], pad
 
 struct AesKey {
   uint32_t rk[60];
@@ -48,13 +49,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
-// fill the workgroup's LDS T-table: word x * 64 + l = Te0[x] (call by all threads, then sync)
+// fill the workgroup's LDS T-tables: Te0[x] of replica r at byte (x << 8) | (r << 2), Te1[x] =
+// ror8 Te0[x] at (x << 8) | 0x80 | (r << 2) (call by all threads, then sync)
 __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
-  for (int i = threadIdx.x; i < kAesLds; i += blockDim.x) lds[i] = te0[i >> 6];
+  for (int i = threadIdx.x; i < kAesLds; i += blockDim.x) {
+    const uint32_t t = te0[i >> 6];
+    lds[i] = (i & 32) ? ror32(t, 8) : t;
+  }
 }
-// stage one key (round keys + IV) in LDS: kKeyWords words
+// stage one key (round keys, IV, round keys rotated left by 16) in LDS: kKeyWords words
 __device__ __forceinline__ void aes_key_fill(uint32_t* dst, const AesKey& k) {
-  for (int i = threadIdx.x; i < kKeyWords; i += blockDim.x) dst[i] = i < 60 ? k.rk[i] : k.iv[i - 60];
+  for (int i = threadIdx.x; i < kKeyWords; i += blockDim.x)
+    dst[i] = i < 60 ? k.rk[i] : i < 64 ? k.iv[i - 60] : i < 124 ? ror32(k.rk[i - 64], 16) : 0u;
 }
 
 // Key sources: a key in LDS (per-lane pointer: lanes may use different keys) or a kernel
@@ -63,44 +69,45 @@ struct LdsKey {
   const uint32_t* p;
   __device__ __forceinline__ uint32_t rk(int i) const { return p[i]; }
   __device__ __forceinline__ uint32_t iv(int i) const { return p[60 + i]; }
+  __device__ __forceinline__ uint32_t rkr(int i) const { return p[64 + i]; }  // rol16(rk[i])
 };
 struct ArgKey {
   const AesKey& k;
   __device__ __forceinline__ uint32_t rk(int i) const { return k.rk[i]; }
   __device__ __forceinline__ uint32_t iv(int i) const { return k.iv[i]; }
+  __device__ __forceinline__ uint32_t rkr(int i) const { return ror32(k.rk[i], 16); }
 };
 
-// T-table lookup of byte `B` of s: the LDS byte offset (byte << 8) | (lane << 2) is one v_perm
-// (byte 1 <- s.byte B, byte 0 <- lane4.byte 0, bytes 2-3 <- 0); bank = lane mod 32, conflict-free
+// T-table lookup of byte `B` of s: the LDS byte offset (byte << 8) | lo is one v_perm (byte 1 <-
+// s.byte B, byte 0 <- lo, bytes 2-3 <- 0) with lo = (lane % 32) << 2 for Te0, | 0x80 for Te1;
+// ds_read_b32 bank = lane % 32: conflict-free
 template <int B>
-__device__ __forceinline__ uint32_t te_b(const uint32_t* lds, uint32_t s, uint32_t lane4) {
-  const uint32_t off = __builtin_amdgcn_perm(s, lane4, 0x0C0C0000u | ((4u + B) << 8));
+__device__ __forceinline__ uint32_t te_b(const uint32_t* lds, uint32_t s, uint32_t lo) {
+  const uint32_t off = __builtin_amdgcn_perm(s, lo, 0x0C0C0000u | ((4u + B) << 8));
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + off);
 }
 
-// AES-256 of the counter block IV + n; returns the 16 keystream bytes as 4 big-endian words
+// AES-256 of the counter block IV + n; returns the 16 keystream bytes as 4 big-endian words.
+// Round column: Te0[a] ^ ror8 Te0[b] ^ ror16 Te0[c] ^ ror24 Te0[d] ^ k
+//             = Te0[a] ^ Te1[b] ^ ror16(Te0[c] ^ Te1[d] ^ rol16 k)   (rotation is linear in ^)
+// = 4 v_perm + 2 v_bitop3 + 1 rotate per column.
 template <class K>
 __device__ __forceinline__ void aes_ctr(const K& key, uint64_t n, const uint32_t* lds, uint32_t out[4]) {
-  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
+  const uint32_t l0 = (threadIdx.x & 31u) << 2, l1 = l0 | 0x80u;
   const uint64_t ivlo = ((uint64_t)key.iv(2) << 32) | key.iv(3), ivhi = ((uint64_t)key.iv(0) << 32) | key.iv(1);
   const uint64_t lo = ivlo + n;
   const uint64_t hi = ivhi + (lo < n ? 1u : 0u);
   uint32_t s0 = (uint32_t)(hi >> 32) ^ key.rk(0), s1 = (uint32_t)hi ^ key.rk(1), s2 = (uint32_t)(lo >> 32) ^ key.rk(2),
            s3 = (uint32_t)lo ^ key.rk(3);
+  auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kr) {
+    return xor3(te_b<3>(lds, a, l0), te_b<2>(lds, b, l1), ror32(xor3(te_b<1>(lds, c, l0), te_b<0>(lds, d, l1), kr), 16));
+  };
 #pragma unroll
   for (int r = 1; r < 14; ++r) {
-    const uint32_t t0 = xor3(xor3(te_b<3>(lds, s0, lane4), ror32(te_b<2>(lds, s1, lane4), 8),
-                                  ror32(te_b<1>(lds, s2, lane4), 16)),
-                             ror32(te_b<0>(lds, s3, lane4), 24), key.rk(4 * r));
-    const uint32_t t1 = xor3(xor3(te_b<3>(lds, s1, lane4), ror32(te_b<2>(lds, s2, lane4), 8),
-                                  ror32(te_b<1>(lds, s3, lane4), 16)),
-                             ror32(te_b<0>(lds, s0, lane4), 24), key.rk(4 * r + 1));
-    const uint32_t t2 = xor3(xor3(te_b<3>(lds, s2, lane4), ror32(te_b<2>(lds, s3, lane4), 8),
-                                  ror32(te_b<1>(lds, s0, lane4), 16)),
-                             ror32(te_b<0>(lds, s1, lane4), 24), key.rk(4 * r + 2));
-    const uint32_t t3 = xor3(xor3(te_b<3>(lds, s3, lane4), ror32(te_b<2>(lds, s0, lane4), 8),
-                                  ror32(te_b<1>(lds, s1, lane4), 16)),
-                             ror32(te_b<0>(lds, s2, lane4), 24), key.rk(4 * r + 3));
+    const uint32_t t0 = col(s0, s1, s2, s3, key.rkr(4 * r));
+    const uint32_t t1 = col(s1, s2, s3, s0, key.rkr(4 * r + 1));
+    const uint32_t t2 = col(s2, s3, s0, s1, key.rkr(4 * r + 2));
+    const uint32_t t3 = col(s3, s0, s1, s2, key.rkr(4 * r + 3));
     s0 = t0;
     s1 = t1;
     s2 = t2;
@@ -108,8 +115,8 @@ __device__ __forceinline__ void aes_ctr(const K& key, uint64_t n, const uint32_t
   }
   // final round: S-box bytes (byte 2 of Te0[x] is S[x]) gathered with v_perm, no MixColumns
   auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-    const uint32_t ab = __builtin_amdgcn_perm(te_b<3>(lds, a, lane4), te_b<2>(lds, b, lane4), 0x06020C0Cu);
-    const uint32_t cd = __builtin_amdgcn_perm(te_b<1>(lds, c, lane4), te_b<0>(lds, d, lane4), 0x0C0C0602u);
+    const uint32_t ab = __builtin_amdgcn_perm(te_b<3>(lds, a, l0), te_b<2>(lds, b, l0), 0x06020C0Cu);
+    const uint32_t cd = __builtin_amdgcn_perm(te_b<1>(lds, c, l0), te_b<0>(lds, d, l0), 0x0C0C0602u);
     return xor3(ab, cd, k);
   };
   out[0] = fin(s0, s1, s2, s3, key.rk(56));

@@ -1421,15 +1421,16 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
 // The deferred TwinCDT tails: wave w resolves segment w, two entries at a time (32 lanes each):
 // each lane sums its share of the exp terms, a 32-lane tree sum decides p < cdf unless p lies
 // within the error bound of both sums, then the terms are summed in the reference's order.
+constexpr int kTailWavesPerSeg = 4;  // waves sharing one segment (latency hiding)
 __global__ __launch_bounds__(256) void cdt_tail_kernel(SampleArgs a) {
   const CdtDev& C = a.cdt_enc;
-  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const long long wv = blockIdx.x;  // segment; its 4 waves take pairs w, w + 4, ...
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31, w = threadIdx.x >> 6;
   const int n = a.tail_n[wv];
   const CdtTail* seg = a.tails + wv * a.tail_cap;
   const double norm = sqrt(2.0 * M_PI) * C.sigma;
   const double two_s2 = 2.0 * C.sigma * C.sigma;
-  for (int e0 = 0; e0 < n; e0 += 2) {
+  for (int e0 = 2 * w; e0 < n; e0 += 2 * kTailWavesPerSeg) {
     const int e = e0 + half < n ? e0 + half : e0;
     const CdtTail t = seg[e];
     double part = 0.0;
@@ -2508,7 +2509,7 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     else
       hipLaunchKernelGGL(cdt_noise_kernel<false>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(false, 0), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
-    hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)(nw / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)nw), dim3(64 * kTailWavesPerSeg), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT tails)"));
     const long long ncos = (long long)batch * (p.cols + p.rows);  // jobs
     const long long wpb = kCosacThreads / 64;
