@@ -292,6 +292,38 @@ rg_status rg_jindo_eval_partial_dev(const rg_jindo* j, const uint64_t* d_ob_enc,
 rg_status rg_jindo_eval_respond_dev(const rg_jindo* j, const uint64_t* d_ob_enc, const uint64_t* d_ob_mlwe,
                                     const uint64_t* d_chals, uint64_t* d_pf_enc, uint64_t* d_pf_mlwe, void* stream);
 
+/* Verifier.Verify (verifier.go:50-282), device-resident, with the Fiat-Shamir challenges
+ * INJECTED as in Evaluate: the caller replays the transcript (SHAKE128 over the commit key,
+ * commitments, x, Proof.Partial; :56-96), encodes the challenges (encodeChallengeTo), computes
+ * leftVec/encode and rightVec (utils.go:63-82) and keeps the shape panics (:51-54).
+ *   d_com   [batch][out_msis][nq][d]  the commitments (rg_jindo_commit_dev layout)
+ *   d_bq, d_bo [batch][nq][d], [batch][nqo][d]  batch[i] / batchOut[i]; NULL when batch == 1
+ *   d_chals [cols][nq][d]   d_left [rows][nq][d] (encode(leftVec(x)[j]))
+ *   d_right [cols*slots][L] rightVec(x)   d_y [batch][L]  the claimed evaluations (Montgomery)
+ *   the Proof: d_pf_incom [dcmp][nqo][d], d_pf_partial [cols+1][nq][d] (Partial, then
+ *   PartialMask), d_pf_enc [rows][nq][d], d_pf_mlwe [in_msis+mlwe][nq][d]  (as Evaluate wrote)
+ *   in_com_dcmp_two_nm, res_two_nm: Parameters.InComDcmpTwoNm() / ResTwoNm() (params.go:432-440)
+ * All four checks run (the reference stops at the first failure; `ok` is the same verdict).
+ * ModUpQtoP (:173) is taken as the centred lift of the ringQOut coefficients (the reading under
+ * which the reference's own TestJindo completes; Lattigo's source is absent: parity unpinned).
+ * Synchronous: returns after the result is on the host. */
+typedef struct {
+  uint64_t outer_norm_sq[10]; /* verifyNorm's nmSq before Sqrt (:263-276), little-endian words */
+  uint64_t inner_norm_sq[10];
+  int outer_ok, inner_ok;     /* Float64(isqrt(nmSq)) < bound (:278-281), decided exactly  */
+  int consistency_ok;         /* verifyConsistency (:203-221)                              */
+  int eval_ok;                /* verifyEval (:224-259)                                     */
+  uint64_t eval_lhs[16];      /* sum right * Decode(Partial) (Montgomery)                  */
+  uint64_t eval_rhs[16];      /* yBatch                                                    */
+  int ok;                     /* Verify's return value                                     */
+} rg_jindo_verify_result;
+rg_status rg_jindo_verify_dev(const rg_jindo* j, size_t batch, const uint64_t* d_com, const uint64_t* d_bq,
+                              const uint64_t* d_bo, const uint64_t* d_chals, const uint64_t* d_left,
+                              const uint64_t* d_right, const uint64_t* d_y, const uint64_t* d_pf_incom,
+                              const uint64_t* d_pf_partial, const uint64_t* d_pf_enc, const uint64_t* d_pf_mlwe,
+                              double in_com_dcmp_two_nm, double res_two_nm, rg_jindo_verify_result* res,
+                              void* stream);
+
 /* ------------------------------------------------------------------------------------ */
 /* Device memory helpers (so a cgo caller needs no HIP headers)                           */
 /* ------------------------------------------------------------------------------------ */

@@ -44,6 +44,13 @@ def lib():
                                       i64p, i64p]
         L.of_uniform_words.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_long,
                                        u64p]
+        L.of_jindo_verify.restype = ctypes.c_int
+        L.of_jindo_verify.argtypes = ([ctypes.c_void_p] + [u64p] * 3 + [ctypes.c_long] + [u64p] * 11 +
+                                      [ctypes.c_double, ctypes.c_double, u64p, ctypes.POINTER(ctypes.c_int), u64p])
+        L.of_jindo_encode_challenge.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, u64p]
+        L.of_jindo_encode.argtypes = [ctypes.c_void_p, u64p, ctypes.c_int, u64p]
+        L.of_norm_below.restype = ctypes.c_int
+        L.of_norm_below.argtypes = [u64p, ctypes.c_double]
     return _LIB
 
 
@@ -287,6 +294,45 @@ class CJindo:
         a = [np.ascontiguousarray(x, dtype=np.uint64) for x in (ob_enc, ob_mlwe, chals)]
         lib().of_jindo_eval_respond(ctypes.c_void_p(self.h), ptr(a[0]), ptr(a[1]), ptr(a[2]), ptr(pe), ptr(pm))
         return pe, pm
+
+    # ---- Verifier.Verify (verifier.go:50-282), challenges injected ----
+    def verify(self, ck, batch, com, bq, bo, chals, left, right, y, pf_incom, pf_partial, pf_enc, pf_mlwe,
+               in_com_dcmp_two_nm, res_two_nm):
+        """Returns dict(ok, flags=[outer, inner, consistency, eval], outer_sq, inner_sq (ints),
+        eval_lhs, eval_rhs (Montgomery limbs)).  bq/bo may be None when batch == 1."""
+        res = np.zeros(20, np.uint64)
+        flags = (ctypes.c_int * 4)()
+        ev = np.zeros(2 * self.L, np.uint64)
+        z = np.zeros(1, np.uint64)
+        a = [np.ascontiguousarray(x, dtype=np.uint64) if x is not None else z
+             for x in (ck[0], ck[1], ck[2], com, bq, bo, chals, left, right, y, pf_incom, pf_partial, pf_enc, pf_mlwe)]
+        ok = lib().of_jindo_verify(ctypes.c_void_p(self.h), ptr(a[0]), ptr(a[1]), ptr(a[2]), ctypes.c_long(batch),
+                                   *[ptr(x) for x in a[3:]], float(in_com_dcmp_two_nm), float(res_two_nm), ptr(res),
+                                   flags, ptr(ev))
+        word = lambda w: sum(int(x) << (64 * i) for i, x in enumerate(w))
+        return dict(ok=bool(ok), flags=[bool(f) for f in flags], outer_sq=word(res[:10]), inner_sq=word(res[10:]),
+                    eval_lhs=ev[:self.L].copy(), eval_rhs=ev[self.L:].copy())
+
+    def encode_challenge(self, ring, b16):
+        """encodeChallengeTo (utils.go:20-46) of 16 bytes into ringQ (ring 0) or ringQOut (1)."""
+        s = self.ps
+        out = np.zeros((s.nqo if ring else s.nq, s.d), np.uint64)
+        lib().of_jindo_encode_challenge(ctypes.c_void_p(self.h), int(ring), bytes(b16), ptr(out))
+        return out
+
+    def encode(self, v):
+        """Encoder.encode (encoder.go:105-117) of <= slots Montgomery elements [n][L]."""
+        s = self.ps
+        out = np.zeros((s.nq, s.d), np.uint64)
+        vv = np.ascontiguousarray(v, dtype=np.uint64)
+        lib().of_jindo_encode(ctypes.c_void_p(self.h), ptr(vv), int(vv.shape[0]), ptr(out))
+        return out
+
+
+def norm_below(S, nm):
+    """oracle.c norm_below: Float64(isqrt(S)) < nm decided by S < K^2 (verifier.go:278-281)"""
+    w = np.array([(S >> (64 * i)) & ((1 << 64) - 1) for i in range(10)], np.uint64)
+    return bool(lib().of_norm_below(ptr(w), float(nm)))
 
 
 def uniform_words(seed, inst, first, n):

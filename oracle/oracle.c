@@ -14,6 +14,7 @@
  *
  * Layouts are identical to the C-ABI in include/ringo.h so tests compare buffers bytewise.
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -860,6 +861,332 @@ void of_jindo_eval_respond(const of_jindo* J, const uint64_t* ob_enc, const uint
         mac_mont(pf_mlwe + (size_t)i * polyq + (size_t)l * d, chals + (size_t)j * polyq + (size_t)l * d,
                  ob_mlwe + ((size_t)j * nm + i) * polyq + (size_t)l * d, &J->rq[l], d);
   }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Verifier.Verify (jindo/verifier.go:50-282) with the Fiat-Shamir challenges injected (the   */
+/* transcript, encodeChallengeTo, leftVec/rightVec/encode stay with the caller, as in          */
+/* Evaluate).  Layouts: include/ringo.h rg_jindo_verify_dev.                                   */
+/* ------------------------------------------------------------------------------------------ */
+#define NW 10 /* words of a sum of squares */
+/* reconstructTo (rns.go:76-105): centred value of one coefficient -> sign + magnitude */
+static void crt_centred(const of_subring* src, int nsrc, const uint64_t* r, int* neg, uint64_t* mag /* [W] */) {
+  int64_t b0 = (int64_t)(r[0] > (src[0].q >> 1) ? r[0] - src[0].q : r[0]);
+  int same = 1;
+  for (int j = 1; j < nsrc; ++j) {
+    int64_t bj = (int64_t)(r[j] > (src[j].q >> 1) ? r[j] - src[j].q : r[j]);
+    if (bj != b0) { same = 0; break; }
+  }
+  if (same) {
+    *neg = b0 < 0;
+    mw_from_u64(mag, *neg ? (uint64_t)(-(b0 + 1)) + 1 : (uint64_t)b0);
+    return;
+  }
+  uint64_t x[4];
+  for (int j = 0; j < nsrc; ++j) {
+    uint64_t q = src[j].q, v = r[j] % q;
+    for (int k = 0; k < j; ++k) {
+      uint64_t xk = x[k] % q;
+      v = v >= xk ? v - xk : v + q - xk;
+      v = mulmod(v, powmod(src[k].q % q, q - 2, q), q);
+    }
+    x[j] = v;
+  }
+  uint64_t V[W], Q[W], Qh[W];
+  mw_from_u64(V, x[nsrc - 1]);
+  for (int j = nsrc - 2; j >= 0; --j) mw_muladd(V, src[j].q, x[j]);
+  mw_from_u64(Q, 1);
+  for (int j = 0; j < nsrc; ++j) mw_muladd(Q, src[j].q, 0);
+  shr_n(Qh, Q, W, 1);
+  *neg = mw_geq(V, Qh);
+  if (*neg)
+    sub_n(mag, Q, V, W);
+  else
+    memcpy(mag, V, 8 * W);
+}
+/* IMForm + INTT of one [n][d] polynomial, in place (verifier.go:99-114) */
+static void inv_poly(const of_jindo* J, const of_subring* R, int n, uint64_t* p) {
+  int d = J->P.d;
+  for (int l = 0; l < n; ++l) {
+    for (int k = 0; k < d; ++k) p[(size_t)l * d + k] = mulmod(p[(size_t)l * d + k], R[l].minv, R[l].q);
+    r_intt(&R[l], p + (size_t)l * d);
+  }
+}
+/* sum of squares of the centred coefficients of npoly NTT+Montgomery polys (verifyNorm :262-276) */
+static void norm_sq_add(const of_jindo* J, const of_subring* R, int n, const uint64_t* polys, long npoly,
+                        size_t stride, uint64_t* acc /* [NW] */) {
+  int d = J->P.d;
+  uint64_t* t = (uint64_t*)malloc(8 * (size_t)n * d);
+  for (long i = 0; i < npoly; ++i) {
+    for (int l = 0; l < n; ++l) memcpy(t + (size_t)l * d, polys + i * stride + (size_t)l * d, 8 * (size_t)d);
+    inv_poly(J, R, n, t);
+    for (int k = 0; k < d; ++k) {
+      uint64_t r[4], mag[W], sq[2 * W];
+      int neg;
+      for (int l = 0; l < n; ++l) r[l] = t[(size_t)l * d + k];
+      crt_centred(R, n, r, &neg, mag);
+      memset(sq, 0, sizeof(sq));
+      for (int a = 0; a < W; ++a) {
+        uint64_t c = 0;
+        for (int b = 0; b < W; ++b) {
+          u128 s2 = (u128)mag[a] * mag[b] + sq[a + b] + c;
+          sq[a + b] = (uint64_t)s2;
+          c = (uint64_t)(s2 >> 64);
+        }
+        sq[a + W] += c;
+      }
+      uint64_t c = 0;
+      for (int w = 0; w < NW; ++w) {
+        u128 s2 = (u128)acc[w] + (w < 2 * W ? sq[w] : 0) + c;
+        acc[w] = (uint64_t)s2;
+        c = (uint64_t)(s2 >> 64);
+      }
+    }
+  }
+  free(t);
+}
+/* nmTest < nm with nmTest = Float64(floor(sqrt(S))) (verifyNorm :278-281), decided exactly:
+   the largest integer T with (double)T < nm is K - 1 where K = the smallest T with (double)T >= nm,
+   so the test is S < K^2.  The double nm = M 2^E (M < 2^53): K = ceil(nm) when nm <= 2^53, else
+   the midpoint below nm, plus one when M is odd (ties round to even). */
+static int norm_below(const uint64_t* S, double nm) {
+  if (!(nm > 0)) return 0;
+  uint64_t K[NW] = {0}, K2[2 * NW];
+  int e;
+  double fr = frexp(nm, &e); /* nm = fr 2^e, fr in [0.5, 1) */
+  uint64_t M = (uint64_t)ldexp(fr, 53);
+  int E = e - 53;
+  if (E <= 0) {
+    double c = ceil(nm);
+    if (c >= 18446744073709551616.0) return 1;
+    K[0] = (uint64_t)c;
+  } else {
+    /* nm = M 2^E; the double below is nm - 2^E, or nm - 2^(E-1) when M = 2^52 */
+    int sub_e = (M == (1ull << 52)) ? E - 2 : E - 1; /* half the gap below */
+    /* K = M 2^E - 2^sub_e (+1 if M odd) */
+    K[E / 64] = M << (E % 64);
+    if (E % 64 && E / 64 + 1 < NW) K[E / 64 + 1] = M >> (64 - E % 64);
+    uint64_t h[NW] = {0};
+    if (sub_e >= 0) h[sub_e / 64] = 1ull << (sub_e % 64);
+    sub_n(K, K, h, NW);
+    if (M & 1) {
+      for (int k = 0; k < NW; ++k) if (++K[k]) break;
+    }
+  }
+  memset(K2, 0, sizeof(K2));
+  for (int a = 0; a < NW; ++a) {
+    uint64_t c = 0;
+    for (int b = 0; b < NW; ++b) {
+      u128 s2 = (u128)K[a] * K[b] + K2[a + b] + c;
+      K2[a + b] = (uint64_t)s2;
+      c = (uint64_t)(s2 >> 64);
+    }
+    K2[a + NW] += c;
+  }
+  for (int w = 2 * NW - 1; w >= NW; --w) if (K2[w]) return 1; /* K^2 exceeds any S */
+  for (int w = NW - 1; w >= 0; --w)
+    if (S[w] != K2[w]) return S[w] < K2[w];
+  return 0;
+}
+int of_norm_below(const uint64_t* S, double nm) { return norm_below(S, nm); }
+/* Decode (encoder.go:203-219) of one NTT+Montgomery ringQ polynomial: nout slots -> Montgomery */
+static void decode_poly(const of_jindo* J, const uint64_t* poly, int nout, uint64_t* out) {
+  const of_jindo_params* P = &J->P;
+  int d = P->d, L = J->F.L, nq = P->nq;
+  uint64_t* t = (uint64_t*)malloc(8 * (size_t)nq * d);
+  uint64_t* ce = (uint64_t*)malloc(8 * (size_t)d * L);
+  memcpy(t, poly, 8 * (size_t)nq * d);
+  inv_poly(J, J->rq, nq, t);
+  uint64_t two32[MAXL], two64[MAXL], bm[MAXL];
+  f_from_u64(&J->F, two32, 1ull << 32);
+  f_mul(&J->F, two64, two32, two32, L);
+  f_from_u64(&J->F, bm, P->base);
+  for (int k = 0; k < d; ++k) { /* SetBigInt of the centred value (element.go SetBigInt: mod p) */
+    uint64_t r[4], mag[W], acc[MAXL] = {0}, wv[MAXL];
+    int neg;
+    for (int l = 0; l < nq; ++l) r[l] = t[(size_t)l * d + k];
+    crt_centred(J->rq, nq, r, &neg, mag);
+    for (int w = W - 1; w >= 0; --w) {
+      f_mul(&J->F, acc, acc, two64, L);
+      f_from_u64(&J->F, wv, mag[w]);
+      f_add(&J->F, acc, acc, wv, L);
+    }
+    if (neg) f_neg(&J->F, acc, acc, L);
+    memcpy(ce + (size_t)k * L, acc, 8 * (size_t)L);
+  }
+  for (int i = 0; i < nout; ++i) {
+    uint64_t v[MAXL] = {0};
+    for (int j = P->exp - 1; j >= 0; --j) {
+      f_mul(&J->F, v, v, bm, L);
+      f_add(&J->F, v, v, ce + (size_t)(j * P->slots + i) * L, L);
+    }
+    memcpy(out + (size_t)i * L, v, 8 * (size_t)L);
+  }
+  free(t);
+  free(ce);
+}
+/* res[0..NW) outer nmSq, res[NW..2NW) inner nmSq, flags[4] = outer, inner, consistency, eval;
+   evals[2][L] = (sum right*dcd, yBatch).  Returns 1 iff all four checks pass. */
+int of_jindo_verify(const of_jindo* J, const uint64_t* ck_in, const uint64_t* ck_mlwe, const uint64_t* ck_out,
+                    long batch, const uint64_t* com, const uint64_t* bq, const uint64_t* bo, const uint64_t* chals,
+                    const uint64_t* left, const uint64_t* right, const uint64_t* y, const uint64_t* pf_incom,
+                    const uint64_t* pf_partial, const uint64_t* pf_enc, const uint64_t* pf_mlwe, double in_com_dcmp_two_nm,
+                    double res_two_nm, uint64_t* res, int* flags, uint64_t* evals) {
+  const of_jindo_params* P = &J->P;
+  const int d = P->d, nq = P->nq, nqo = P->nqo, nm = P->in_msis + P->mlwe, L = J->F.L;
+  const size_t polyq = (size_t)nq * d, polyo = (size_t)nqo * d;
+  memset(res, 0, 8 * 2 * NW);
+  /* verifyOuterCommitment (:136-161) */
+  norm_sq_add(J, J->ro, nqo, pf_incom, P->dcmp, polyo, res);
+  uint64_t* c = (uint64_t*)malloc(8 * polyq);
+  for (int i = 0; i < P->out_msis; ++i) {
+    for (int l = 0; l < nqo; ++l) {
+      const of_subring* S = &J->ro[l];
+      uint64_t* a = c + (size_t)l * d;
+      if (batch > 1) {
+        memset(a, 0, 8 * (size_t)d);
+        for (long j = 0; j < batch; ++j)
+          mac_mont(a, com + ((size_t)j * P->out_msis + i) * polyq + (size_t)l * d, bo + (size_t)j * polyo + (size_t)l * d, S, d);
+      } else {
+        memcpy(a, com + (size_t)i * polyq + (size_t)l * d, 8 * (size_t)d);
+      }
+      uint64_t cut = powmod(2, (uint64_t)P->log_out_cut, S->q); /* MulRNSScalarMontgomery(MForm(2^cut)) */
+      for (int k = 0; k < d; ++k) a[k] = mulmod(a[k], cut, S->q);
+      uint64_t* b = (uint64_t*)calloc((size_t)d, 8);
+      for (int j = 0; j < P->dcmp; ++j)
+        mac_mont(b, ck_out + (((size_t)i * P->dcmp + j) * nqo + l) * d, pf_incom + (size_t)j * polyo + (size_t)l * d, S, d);
+      for (int k = 0; k < d; ++k) a[k] = a[k] >= b[k] ? a[k] - b[k] : a[k] + S->q - b[k]; /* ...ThenSub */
+      free(b);
+    }
+    norm_sq_add(J, J->ro, nqo, c, 1, polyo, res);
+  }
+  flags[0] = norm_below(res, in_com_dcmp_two_nm);
+  /* verifyInnerCommitment (:164-200) */
+  uint64_t* lift = (uint64_t*)malloc(8 * polyq * (size_t)P->dcmp);
+  {
+    uint64_t* t = (uint64_t*)malloc(8 * polyo);
+    for (int j = 0; j < P->dcmp; ++j) { /* MForm(NTT(ModUpQtoP(pfInv.InCommit[j]))): centred lift */
+      memcpy(t, pf_incom + (size_t)j * polyo, 8 * polyo);
+      round_poly(J, J->ro, nqo, t, 0, J->rq, nq, lift + (size_t)j * polyq);
+    }
+    free(t);
+  }
+  norm_sq_add(J, J->rq, nq, pf_enc, P->rows, polyq, res + NW);
+  norm_sq_add(J, J->rq, nq, pf_mlwe, nm, polyq, res + NW);
+  for (int i = 0; i < P->in_msis; ++i) {
+    for (int l = 0; l < nq; ++l) {
+      const of_subring* S = &J->rq[l];
+      uint64_t* a = c + (size_t)l * d;
+      memset(a, 0, 8 * (size_t)d);
+      for (int j = 0; j <= P->cols; ++j) {
+        const uint64_t* lj = lift + (size_t)(j * P->in_msis + i) * polyq + (size_t)l * d;
+        if (j == P->cols) {
+          for (int k = 0; k < d; ++k) { a[k] += lj[k]; if (a[k] >= S->q) a[k] -= S->q; }
+        } else {
+          mac_mont(a, lj, chals + (size_t)j * polyq + (size_t)l * d, S, d);
+        }
+      }
+      uint64_t cut = powmod(2, (uint64_t)P->log_in_cut, S->q);
+      for (int k = 0; k < d; ++k) a[k] = mulmod(a[k], cut, S->q);
+      uint64_t* b = (uint64_t*)calloc((size_t)d, 8);
+      for (int j = 0; j < P->rows; ++j)
+        mac_mont(b, ck_in + (((size_t)i * P->rows + j) * nq + l) * d, pf_enc + (size_t)j * polyq + (size_t)l * d, S, d);
+      for (int j = 0; j < P->mlwe; ++j)
+        mac_mont(b, ck_mlwe + (((size_t)i * P->mlwe + j) * nq + l) * d, pf_mlwe + (size_t)j * polyq + (size_t)l * d, S, d);
+      const uint64_t* e = pf_mlwe + (size_t)(P->mlwe + i) * polyq + (size_t)l * d;
+      for (int k = 0; k < d; ++k) {
+        uint64_t bk = b[k] + e[k];
+        if (bk >= S->q) bk -= S->q;
+        a[k] = a[k] >= bk ? a[k] - bk : a[k] + S->q - bk;
+      }
+      free(b);
+    }
+    norm_sq_add(J, J->rq, nq, c, 1, polyq, res + NW);
+  }
+  free(lift);
+  flags[1] = norm_below(res + NW, res_two_nm);
+  /* verifyConsistency (:203-221) */
+  int consistent = 1;
+  for (int l = 0; l < nq; ++l) {
+    const of_subring* S = &J->rq[l];
+    uint64_t* a = c + (size_t)l * d;
+    uint64_t* b = (uint64_t*)calloc((size_t)d, 8);
+    memset(a, 0, 8 * (size_t)d);
+    for (int i = 0; i < P->rows; ++i)
+      mac_mont(a, left + (size_t)i * polyq + (size_t)l * d, pf_enc + (size_t)i * polyq + (size_t)l * d, S, d);
+    for (int i = 0; i < P->cols; ++i)
+      mac_mont(b, chals + (size_t)i * polyq + (size_t)l * d, pf_partial + (size_t)i * polyq + (size_t)l * d, S, d);
+    const uint64_t* pm = pf_partial + (size_t)P->cols * polyq + (size_t)l * d;
+    for (int k = 0; k < d; ++k) {
+      uint64_t bk = b[k] + pm[k];
+      if (bk >= S->q) bk -= S->q;
+      consistent &= a[k] == bk;
+    }
+    free(b);
+  }
+  free(c);
+  flags[2] = consistent;
+  /* verifyEval (:224-259) */
+  uint64_t* dcd = (uint64_t*)malloc(8 * (size_t)P->slots * L);
+  uint64_t lhs[MAXL] = {0}, rhs[MAXL] = {0}, t[MAXL];
+  for (int i = 0; i < P->cols; ++i) {
+    decode_poly(J, pf_partial + (size_t)i * polyq, P->slots, dcd);
+    for (int j = 0; j < P->slots; ++j) {
+      f_mul(&J->F, t, right + (size_t)(i * P->slots + j) * L, dcd + (size_t)j * L, L);
+      f_add(&J->F, lhs, lhs, t, L);
+    }
+  }
+  if (batch > 1) {
+    for (long i = 0; i < batch; ++i) {
+      decode_poly(J, bq + (size_t)i * polyq, 1, dcd);
+      f_mul(&J->F, t, dcd, y + (size_t)i * L, L);
+      f_add(&J->F, rhs, rhs, t, L);
+    }
+  } else {
+    memcpy(rhs, y, 8 * (size_t)L);
+  }
+  free(dcd);
+  memcpy(evals, lhs, 8 * (size_t)L);
+  memcpy(evals + L, rhs, 8 * (size_t)L);
+  flags[3] = memcmp(lhs, rhs, 8 * (size_t)L) == 0;
+  return flags[0] && flags[1] && flags[2] && flags[3];
+}
+
+/* encodeChallengeTo (utils.go:20-46) into one ring: coefficient i*slots <- signed digit i of the
+   128-bit challenge in base ChallengeBound; then MForm and NTT.  ring = 0: ringQ, 1: ringQOut */
+void of_jindo_encode_challenge(const of_jindo* J, int ring, const unsigned char* bytes16, uint64_t* out) {
+  const of_jindo_params* P = &J->P;
+  const of_subring* R = ring ? J->ro : J->rq;
+  const int n = ring ? P->nqo : P->nq, d = P->d;
+  uint64_t c[2] = {0, 0};
+  for (int i = 0; i < 8; ++i) {
+    c[0] = (c[0] << 8) | bytes16[i];
+    c[1] = (c[1] << 8) | bytes16[8 + i];
+  }
+  uint64_t bnd = P->base < (1ull << (120 / P->exp)) ? P->base : (1ull << (120 / P->exp));
+  bnd /= 2; /* ChallengeBound (params.go:357-360) */
+  memset(out, 0, 8 * (size_t)n * d);
+  for (int i = 0; i < P->exp; ++i) {
+    uint64_t r = 0; /* divMod64 over [c0, c1] little-endian words */
+    for (int k = 1; k >= 0; --k) {
+      u128 num = ((u128)r << 64) | c[k];
+      c[k] = (uint64_t)(num / bnd);
+      r = (uint64_t)(num % bnd);
+    }
+    for (int l = 0; l < n; ++l) out[(size_t)l * d + (size_t)i * P->slots] = r > bnd / 2 ? R[l].q - (bnd - r) : r;
+  }
+  for (int l = 0; l < n; ++l) {
+    uint64_t* p = out + (size_t)l * d;
+    for (int k = 0; k < d; ++k) p[k] = mulmod(p[k], R[l].m, R[l].q);
+    r_ntt(&R[l], p);
+  }
+}
+
+/* Encoder.encode (encoder.go:105-117) of n <= slots Montgomery elements: ringQ NTT+Mont poly */
+void of_jindo_encode(const of_jindo* J, const uint64_t* v, int n, uint64_t* out) {
+  int64_t* zero = (int64_t*)calloc((size_t)J->P.d, 8);
+  rand_encode(J, out, v, n, zero); /* no noise: MForm(digits), NTT */
+  free(zero);
 }
 
 /* ------------------------------------------------------------------------------------------ */

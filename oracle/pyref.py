@@ -617,6 +617,8 @@ class JindoParams:
                     mask_blind_sd=mask_blind_sd / math.sqrt(2 * math.pi),
                     mlwe_sd=mlwe_sd / math.sqrt(2 * math.pi),
                     mask_mlwe_sd=mask_mlwe_sd / math.sqrt(2 * math.pi),
+                    res_two_nm=res_two + in_cut_two,
+                    in_com_dcmp_two_nm=in_dcmp_two + out_cut_two,
                 )
             nn <<= 1
         self.__dict__.update(best)
@@ -624,7 +626,8 @@ class JindoParams:
     def as_dict(self):
         keys = ["batch", "rank", "rows", "cols", "base", "exp", "slots", "d", "in_msis",
                 "out_msis", "mlwe", "log_in_cut", "log_out_cut", "in_com_dcmp_len", "q", "qo",
-                "ecd_sd", "ecd_blind_sd", "mask_sd", "mask_blind_sd", "mlwe_sd", "mask_mlwe_sd"]
+                "ecd_sd", "ecd_blind_sd", "mask_sd", "mask_blind_sd", "mlwe_sd", "mask_mlwe_sd",
+                "res_two_nm", "in_com_dcmp_two_nm"]
         return {k: getattr(self, k) for k in keys}
 
 

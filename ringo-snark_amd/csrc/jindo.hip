@@ -910,6 +910,49 @@ __device__ __forceinline__ void mw_muladd(uint64_t* v, int nw, uint64_t m, uint6
   }
 }
 
+// reconstructTo (rns.go:76-105) of one coefficient's residues r[ns] (coefficient domain): the
+// centred value as sign (returned) and 4-word magnitude
+__device__ __forceinline__ bool crt_centred(const CrtDev& crt, int ns, const uint64_t* r, uint64_t mag[4]) {
+  bool neg;
+  mag[0] = mag[1] = mag[2] = mag[3] = 0;
+  if (ns == 1) {  // reconstructTo fast path: toBalanced (rns.go:68-73,78-91)
+    const uint64_t q = crt.q[0];
+    neg = r[0] > (q >> 1);
+    mag[0] = neg ? q - r[0] : r[0];
+  } else {  // Garner: V = x0 + q0 (x1 + q1 (x2 + ...)) in [0, Q)  (rns.go:93-99)
+    uint64_t x[kMaxQ];
+    for (int j = 0; j < ns; ++j) {
+      const uint64_t qj = crt.q[j];
+      uint64_t v = r[j];
+      for (int kk = 0; kk < j; ++kk) {
+        uint64_t xk = x[kk];
+        if (xk >= qj) xk = (xk - qj >= qj) ? xk % qj : xk - qj;  // ring primes share a bit size
+        v = mod_sub(v, xk, qj);
+        v = sh_mul(v, crt.inv[j][kk], crt.inv_sh[j][kk], qj);
+      }
+      x[j] = v;
+    }
+    uint64_t V[4] = {x[ns - 1], 0, 0, 0};
+    for (int j = ns - 2; j >= 0; --j) mw_muladd(V, 4, crt.q[j], x[j]);
+    // V >= floor(Q/2) -> V - Q (rns.go:100-102)
+    bool ge = true;
+    for (int i = 3; i >= 0; --i) {
+      if (V[i] != crt.Qhalf[i]) {
+        ge = V[i] > crt.Qhalf[i];
+        break;
+      }
+    }
+    neg = ge;
+    if (neg) {
+      uint32_t br = 0;
+      for (int i = 0; i < 4; ++i) mag[i] = subb(crt.Q[i], V[i], br);
+    } else {
+      for (int i = 0; i < 4; ++i) mag[i] = V[i];
+    }
+  }
+  return neg;
+}
+
 __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
   // LDS sized per launch (max(ns, nd) limbs x d words), not for kMaxQ x kMaxD: occupancy is then
   // register-limited (7 waves/SIMD) instead of LDS-limited (5)
@@ -935,43 +978,8 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
   for (int k = tid; k < d; k += blockDim.x) {
     uint64_t r[kMaxQ];
     for (int l = 0; l < ns; ++l) r[l] = poly(l)[k];
-    bool neg;
-    uint64_t mag[4] = {0, 0, 0, 0};
-    if (ns == 1) {  // reconstructTo fast path: toBalanced (rns.go:68-73,78-91)
-      const uint64_t q = a.crt.q[0];
-      neg = r[0] > (q >> 1);
-      mag[0] = neg ? q - r[0] : r[0];
-    } else {  // Garner: V = x0 + q0 (x1 + q1 (x2 + ...)) in [0, Q)  (rns.go:93-99)
-      uint64_t x[kMaxQ];
-      for (int j = 0; j < ns; ++j) {
-        const uint64_t qj = a.crt.q[j];
-        uint64_t v = r[j];
-        for (int kk = 0; kk < j; ++kk) {
-          uint64_t xk = x[kk];
-          if (xk >= qj) xk = (xk - qj >= qj) ? xk % qj : xk - qj;  // ring primes share a bit size
-          v = mod_sub(v, xk, qj);
-          v = sh_mul(v, a.crt.inv[j][kk], a.crt.inv_sh[j][kk], qj);
-        }
-        x[j] = v;
-      }
-      uint64_t V[4] = {x[ns - 1], 0, 0, 0};
-      for (int j = ns - 2; j >= 0; --j) mw_muladd(V, 4, a.crt.q[j], x[j]);
-      // V >= floor(Q/2) -> V - Q (rns.go:100-102)
-      bool ge = true;
-      for (int i = 3; i >= 0; --i) {
-        if (V[i] != a.crt.Qhalf[i]) {
-          ge = V[i] > a.crt.Qhalf[i];
-          break;
-        }
-      }
-      neg = ge;
-      if (neg) {
-        uint32_t br = 0;
-        for (int i = 0; i < 4; ++i) mag[i] = subb(a.crt.Q[i], V[i], br);
-      } else {
-        for (int i = 0; i < 4; ++i) mag[i] = V[i];
-      }
-    }
+    uint64_t mag[4];
+    bool neg = crt_centred(a.crt, ns, r, mag);
     // floor(value / 2^cut) (big.Int.Rsh on a signed value rounds toward -inf)
     bool lost = false;
     int cut = a.cut;
@@ -1903,6 +1911,199 @@ __global__ __launch_bounds__(512) void uniform_words_kernel(AesKey key, const ui
   u.init(kl, lds, inst);
   out[gid] = u.word_at(first + (unsigned long long)gid);
 }
+// ------------------------------------------------------------------------------------------
+// 7. Verifier.Verify (verifier.go:50-282), challenges injected.  The MACs run on mac_kernel,
+// the lifted inner commitments on round_kernel (cut 0, ringQOut -> ringQ); these kernels add:
+//   norm_kernel    workgroup per polynomial: IMForm, INTT, centred CRT, sum of squares
+//                  (verifyNorm :262-276) -> kNormW words per polynomial
+//   combine_kernel A * 2^cut - B per residue (MulRNSScalarMontgomery, ...ThenSub)
+//   neq_kernel     any word of x != y -> flag (verifyConsistency :203-221)
+//   decode_kernel  workgroup per polynomial: IMForm, INTT, centred CRT, SetBigInt mod p,
+//                  Horner in base b over the slots (DecodeTo, encoder.go:203-219)
+//   dot2_kernel    one workgroup: sum right * dcd and sum batchDcd[0] * y (verifyEval :224-259)
+// ------------------------------------------------------------------------------------------
+constexpr int kNormW = 10;  // words of a sum of squares (|value| < 2^240, <= 2^20 values)
+
+struct NormArgs {
+  int d;
+  RingDev R;
+  CrtDev crt;
+  const uint64_t* in;  // [npoly] at stride in_stride, R.n limbs
+  long long in_stride;
+  uint64_t* out;       // [npoly][kNormW]
+};
+
+__device__ __forceinline__ void mw_add(uint64_t* a, const uint64_t* b, int n) {
+  uint32_t c = 0;
+  for (int i = 0; i < n; ++i) a[i] = addc(a[i], b[i], c);
+}
+
+__global__ __launch_bounds__(256) void norm_kernel(NormArgs a) {
+  extern __shared__ uint64_t poly_lds[];
+  const int d = a.d, tid = threadIdx.x, ns = a.R.n;
+  auto poly = [&](int l) { return poly_lds + (long long)l * d; };
+  const long long pid = blockIdx.x;
+  const uint64_t* in = a.in + pid * a.in_stride;
+  for (int k = tid; k < ns * d; k += blockDim.x) {
+    const int l = k / d;
+    const RnsPrime& P = a.R.p[l];
+    poly(l)[k % d] = sh_mul(in[k], P.rinv, P.rinv_sh, P.q);  // IMForm
+  }
+  __syncthreads();
+  const int half = blockDim.x >> 1;
+  for (int l0 = 0; l0 < ns; l0 += 2) {
+    const int l = l0 + (tid >= half ? 1 : 0);
+    const bool active = l < ns;
+    const int lc = active ? l : l0;
+    intt_lds(poly(lc), d, a.R.bwd + (long long)lc * d, a.R.p[lc], tid % half, half, active);
+  }
+  uint64_t acc[kNormW];
+  for (int i = 0; i < kNormW; ++i) acc[i] = 0;
+  for (int k = tid; k < d; k += blockDim.x) {
+    uint64_t r[kMaxQ], mag[4];
+    for (int l = 0; l < ns; ++l) r[l] = poly(l)[k];
+    crt_centred(a.crt, ns, r, mag);
+    uint64_t sq[kNormW];
+    for (int i = 0; i < kNormW; ++i) sq[i] = 0;
+    for (int i = 0; i < 4; ++i) {
+      uint64_t carry = 0;
+      for (int j = 0; j < 4; ++j) {
+        uint64_t lo, hi;
+        mul_wide(mag[i], mag[j], lo, hi);
+        uint32_t c = 0;
+        lo = addc(lo, sq[i + j], c);
+        hi += c;
+        c = 0;
+        lo = addc(lo, carry, c);
+        hi += c;
+        sq[i + j] = lo;
+        carry = hi;
+      }
+      sq[i + 4] += carry;
+    }
+    mw_add(acc, sq, kNormW);
+  }
+  __syncthreads();  // poly_lds is reused for the reduction
+  for (int i = 0; i < kNormW; ++i) poly_lds[tid * kNormW + i] = acc[i];
+  __syncthreads();
+  for (int s = blockDim.x >> 1; s > 0; s >>= 1) {
+    if (tid < s) mw_add(poly_lds + tid * kNormW, poly_lds + (tid + s) * kNormW, kNormW);
+    __syncthreads();
+  }
+  if (tid < kNormW) a.out[pid * kNormW + tid] = poly_lds[tid];
+}
+
+// out[p][l][k] = A[p][l][k] * c_l - B[p][l][k] mod q_l  (A, B, out: [npoly][nl][d] contiguous)
+__global__ __launch_bounds__(256) void combine_kernel(const uint64_t* A, const uint64_t* B, uint64_t* out,
+                                                      long long n, int nl, int d, RingDev R, uint64_t c0,
+                                                      uint64_t c1, uint64_t c2, uint64_t c3) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int l = (int)((i / d) % nl);
+  const RnsPrime& P = R.p[l];
+  const uint64_t c = l == 0 ? c0 : l == 1 ? c1 : l == 2 ? c2 : c3;
+  const uint64_t cp = (uint64_t)(((unsigned __int128)c << 64) / P.q);
+  out[i] = mod_sub(sh_mul(A[i], c, cp, P.q), B[i], P.q);
+}
+
+__global__ __launch_bounds__(256) void neq_kernel(const uint64_t* x, const uint64_t* y, long long n, int* flag) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && x[i] != y[i]) atomicOr(flag, 1);
+}
+
+template <int L>
+struct DecodeArgs {
+  int d, slots, exp, nout;
+  RingDev R;
+  CrtDev crt;
+  FieldParams<L> F;
+  uint64_t pw[4][L];  // 2^(64 i) R^2 mod p: montmul(w, pw[i]) = w 2^(64 i) R
+  uint64_t bmont[L];  // base in Montgomery form
+  const uint64_t* in;  // [npoly][R.n][d]
+  uint64_t* out;       // [npoly][nout][L]
+};
+
+template <int L>
+__global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<L> a) {
+  extern __shared__ uint64_t poly_lds[];  // R.n * d words, then d * L words of coefficients
+  const int d = a.d, tid = threadIdx.x, ns = a.R.n;
+  auto poly = [&](int l) { return poly_lds + (long long)l * d; };
+  uint64_t* ce = poly_lds + (long long)ns * d;
+  const long long pid = blockIdx.x;
+  const uint64_t* in = a.in + pid * ns * d;
+  for (int k = tid; k < ns * d; k += blockDim.x) {
+    const int l = k / d;
+    const RnsPrime& P = a.R.p[l];
+    poly(l)[k % d] = sh_mul(in[k], P.rinv, P.rinv_sh, P.q);  // IMForm
+  }
+  __syncthreads();
+  const int half = blockDim.x >> 1;
+  for (int l0 = 0; l0 < ns; l0 += 2) {
+    const int l = l0 + (tid >= half ? 1 : 0);
+    const bool active = l < ns;
+    const int lc = active ? l : l0;
+    intt_lds(poly(lc), d, a.R.bwd + (long long)lc * d, a.R.p[lc], tid % half, half, active);
+  }
+  for (int k = tid; k < d; k += blockDim.x) {  // reconstructTo, then SetBigInt (mod p)
+    uint64_t r[kMaxQ], mag[4];
+    for (int l = 0; l < ns; ++l) r[l] = poly(l)[k];
+    const bool neg = crt_centred(a.crt, ns, r, mag);
+    uint64_t v[L], t[L], w[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) v[i] = 0;
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) w[j] = j == 0 ? mag[i] : 0;
+      if (L == 1) w[0] = mag[i] % a.F.q[0];  // a word may exceed a one-limb p
+      f_mul<L>(t, w, a.pw[i], a.F);
+      f_add<L>(v, v, t, a.F);
+    }
+    if (neg) f_neg<L>(v, v, a.F);
+#pragma unroll
+    for (int j = 0; j < L; ++j) ce[(long long)k * L + j] = v[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < a.nout; i += blockDim.x) {  // Horner over j = exp-1 .. 0
+    uint64_t v[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) v[j] = 0;
+    for (int j = a.exp - 1; j >= 0; --j) {
+      f_mul<L>(v, v, a.bmont, a.F);
+      f_add<L>(v, v, ce + (long long)(j * a.slots + i) * L, a.F);
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) a.out[(pid * a.nout + i) * L + j] = v[j];
+  }
+}
+
+// one workgroup: out[0] = sum_i x1[i] * y1[i] (n1 terms), out[1] = sum_i x2[i] * y2[i] (n2)
+template <int L>
+__global__ __launch_bounds__(256) void dot2_kernel(FieldParams<L> F, const uint64_t* x1, const uint64_t* y1,
+                                                   long long n1, const uint64_t* x2, const uint64_t* y2, long long n2,
+                                                   uint64_t* out) {
+  __shared__ uint64_t red[256 * L];
+  for (int which = 0; which < 2; ++which) {
+    const uint64_t* x = which ? x2 : x1;
+    const uint64_t* y = which ? y2 : y1;
+    const long long n = which ? n2 : n1;
+    uint64_t acc[L], t[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = 0;
+    for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+      f_mul<L>(t, x + i * L, y + i * L, F);
+      f_add<L>(acc, acc, t, F);
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) red[threadIdx.x * L + j] = acc[j];
+    __syncthreads();
+    for (int s = blockDim.x >> 1; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s) f_add<L>(red + threadIdx.x * L, red + threadIdx.x * L, red + (threadIdx.x + s) * L, F);
+      __syncthreads();
+    }
+    if (threadIdx.x < L) out[which * L + threadIdx.x] = red[threadIdx.x];
+    __syncthreads();
+  }
+}
 }  // namespace rg
 
 // ------------------------------------------------------------------------------------------
@@ -1936,7 +2137,7 @@ struct rg_jindo {
   rg::RnsPrime rq[rg::kMaxQ], ro[rg::kMaxQ];
   rg::DevBuf rootsq_f, rootsq_b, rootso_f, rootso_b;
   rg::CrtDev crt_q, crt_o;
-  rg::DstDev dst_o;
+  rg::DstDev dst_o, dst_q;
   rg::DevBuf ck_in, ck_mlwe, ck_out;  // the commit key, device-resident (entities.go:21-73 layouts)
   rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3_kernel (inner, outer)
   bool mac3_q = false, mac3_o = false;
@@ -2150,6 +2351,7 @@ static rg_status build(rg_jindo* J) {
   make_crt(p.q, p.nq, J->crt_q);
   make_crt(p.qo, p.nqo, J->crt_o);
   make_dst(p.qo, p.nqo, J->dst_o);
+  make_dst(p.q, p.nq, J->dst_q);
   J->base_inv = (uint64_t)(((unsigned __int128)1 << 64) / p.base);
   return RG_OK;
 }
@@ -2604,6 +2806,145 @@ __global__ __launch_bounds__(256) void rns_reduce_kernel(uint64_t* x, long long 
 
 using namespace rg;
 
+// ---- Verifier.Verify (verifier.go:50-282) ----------------------------------------------------
+// nmTest < nm with nmTest = Float64(isqrt(S)) (verifyNorm :278-281), decided exactly: the test is
+// S < K^2 with K the smallest integer whose float64 is >= nm (ceil(nm) up to 2^53; above, the
+// midpoint below nm, + 1 when nm's mantissa is odd, as ties round to even).
+static bool norm_below(const uint64_t* S, double nm) {
+  constexpr int NW = kNormW;
+  if (!(nm > 0)) return false;
+  uint64_t K[NW] = {0}, K2[2 * NW] = {0};
+  int e;
+  const double fr = frexp(nm, &e);
+  const uint64_t M = (uint64_t)ldexp(fr, 53);
+  const int E = e - 53;
+  if (E <= 0) {
+    const double c = ceil(nm);
+    if (c >= 18446744073709551616.0) return true;
+    K[0] = (uint64_t)c;
+  } else {
+    if (E / 64 >= NW) return true;
+    const int sub_e = (M == (1ull << 52)) ? E - 2 : E - 1;  // half the gap to the double below
+    K[E / 64] = M << (E % 64);
+    if (E % 64 && E / 64 + 1 < NW) K[E / 64 + 1] = M >> (64 - E % 64);
+    uint64_t h[NW] = {0};
+    if (sub_e >= 0) h[sub_e / 64] = 1ull << (sub_e % 64);
+    HostField::sub_n(K, K, h, NW);
+    if (M & 1)
+      for (int k = 0; k < NW; ++k)
+        if (++K[k]) break;
+  }
+  for (int a = 0; a < NW; ++a) {
+    uint64_t c = 0;
+    for (int b = 0; b < NW; ++b) {
+      const unsigned __int128 t = (unsigned __int128)K[a] * K[b] + K2[a + b] + c;
+      K2[a + b] = (uint64_t)t;
+      c = (uint64_t)(t >> 64);
+    }
+    K2[a + NW] += c;
+  }
+  for (int w = 2 * NW - 1; w >= NW; --w)
+    if (K2[w]) return true;
+  for (int w = NW - 1; w >= 0; --w)
+    if (S[w] != K2[w]) return S[w] < K2[w];
+  return false;
+}
+
+template <int L>
+static rg_status launch_decode(const rg_jindo* J, const uint64_t* in, long long npoly, int nout, uint64_t* out,
+                               hipStream_t st) {
+  if (npoly == 0) return RG_OK;
+  const rg_jindo_params& p = J->p;
+  DecodeArgs<L> a;
+  memset(&a, 0, sizeof(a));
+  a.d = p.d;
+  a.slots = p.slots;
+  a.exp = p.exp;
+  a.nout = nout;
+  a.R = ring_dev(J->rq, p.nq, J->rootsq_f, J->rootsq_b);
+  a.crt = J->crt_q;
+  memcpy(a.F.q, J->field.q, 8 * L);
+  a.F.qinv = J->field.qinv;
+  const HostField H(&J->field);
+  uint64_t t32[16], t64[16];
+  H.from_u64(t32, 1ull << 32);
+  H.mul(t64, t32, t32);  // Montgomery form of 2^64
+  memcpy(a.pw[0], J->field.r2, 8 * L);
+  for (int i = 1; i < 4; ++i) H.mul(a.pw[i], a.pw[i - 1], t64);
+  H.from_u64(a.bmont, p.base);
+  a.in = in;
+  a.out = out;
+  const size_t lds = ((size_t)p.nq * p.d + (size_t)p.d * L) * 8;
+  hipLaunchKernelGGL(decode_kernel<L>, dim3((unsigned)npoly), dim3(256), lds, st, a);
+  return check_launch("jindo decode");
+}
+
+template <int L>
+static rg_status launch_dot2(const rg_jindo* J, const uint64_t* x1, const uint64_t* y1, long long n1,
+                             const uint64_t* x2, const uint64_t* y2, long long n2, uint64_t* out, hipStream_t st) {
+  FieldParams<L> F;
+  memcpy(F.q, J->field.q, 8 * L);
+  F.qinv = J->field.qinv;
+  hipLaunchKernelGGL(dot2_kernel<L>, dim3(1), dim3(256), 0, st, F, x1, y1, n1, x2, y2, n2, out);
+  return check_launch("jindo dot");
+}
+
+static rg_status decode_any(const rg_jindo* J, const uint64_t* in, long long npoly, int nout, uint64_t* out,
+                            hipStream_t st) {
+  switch (J->p.field_limbs) {
+    case 1: return launch_decode<1>(J, in, npoly, nout, out, st);
+    case 2: return launch_decode<2>(J, in, npoly, nout, out, st);
+    case 4: return launch_decode<4>(J, in, npoly, nout, out, st);
+    case 7: return launch_decode<7>(J, in, npoly, nout, out, st);
+    default: return launch_decode<14>(J, in, npoly, nout, out, st);
+  }
+}
+static rg_status dot2_any(const rg_jindo* J, const uint64_t* x1, const uint64_t* y1, long long n1, const uint64_t* x2,
+                          const uint64_t* y2, long long n2, uint64_t* out, hipStream_t st) {
+  switch (J->p.field_limbs) {
+    case 1: return launch_dot2<1>(J, x1, y1, n1, x2, y2, n2, out, st);
+    case 2: return launch_dot2<2>(J, x1, y1, n1, x2, y2, n2, out, st);
+    case 4: return launch_dot2<4>(J, x1, y1, n1, x2, y2, n2, out, st);
+    case 7: return launch_dot2<7>(J, x1, y1, n1, x2, y2, n2, out, st);
+    default: return launch_dot2<14>(J, x1, y1, n1, x2, y2, n2, out, st);
+  }
+}
+
+static rg_status launch_norm(const rg_jindo* J, bool outer, const uint64_t* in, long long npoly, long long stride,
+                             uint64_t* out, hipStream_t st) {
+  if (npoly == 0) return RG_OK;
+  const rg_jindo_params& p = J->p;
+  NormArgs a;
+  memset(&a, 0, sizeof(a));
+  a.d = p.d;
+  a.R = outer ? ring_dev(J->ro, p.nqo, J->rootso_f, J->rootso_b) : ring_dev(J->rq, p.nq, J->rootsq_f, J->rootsq_b);
+  a.crt = outer ? J->crt_o : J->crt_q;
+  a.in = in;
+  a.in_stride = stride;
+  a.out = out;
+  const size_t lds = std::max((size_t)a.R.n * p.d, (size_t)256 * kNormW) * 8;
+  hipLaunchKernelGGL(norm_kernel, dim3((unsigned)npoly), dim3(256), lds, st, a);
+  return check_launch("jindo norm");
+}
+
+static rg_status launch_combine(const RnsPrime* P, int nl, int d, int cut, const uint64_t* A, const uint64_t* B,
+                                uint64_t* out, long long npoly, hipStream_t st) {
+  uint64_t c[4] = {0, 0, 0, 0};
+  RingDev R;
+  memset(&R, 0, sizeof(R));
+  R.n = nl;
+  for (int l = 0; l < nl; ++l) {
+    R.p[l] = P[l];
+    unsigned __int128 x = 1;
+    for (int i = 0; i < cut; ++i) x = (x * 2) % P[l].q;  // 2^cut mod q
+    c[l] = (uint64_t)x;
+  }
+  const long long n = npoly * nl * d;
+  hipLaunchKernelGGL(combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, B, out, n, nl, d, R, c[0],
+                     c[1], c[2], c[3]);
+  return check_launch("jindo combine");
+}
+
 extern "C" {
 
 rg_status rg_jindo_eval_batch_dev(const rg_jindo* J, size_t batch, const uint64_t* d_incom, const uint64_t* d_enc,
@@ -2644,6 +2985,158 @@ rg_status rg_jindo_eval_respond_dev(const rg_jindo* J, const uint64_t* d_ob_enc,
   return launch_mac(m, st);
 }
 
+
+rg_status rg_jindo_verify_dev(const rg_jindo* J, size_t batch, const uint64_t* d_com, const uint64_t* d_bq,
+                              const uint64_t* d_bo, const uint64_t* d_chals, const uint64_t* d_left,
+                              const uint64_t* d_right, const uint64_t* d_y, const uint64_t* d_pf_incom,
+                              const uint64_t* d_pf_partial, const uint64_t* d_pf_enc, const uint64_t* d_pf_mlwe,
+                              double in_com_dcmp_two_nm, double res_two_nm, rg_jindo_verify_result* res,
+                              void* stream) {
+  if (!J || !res || !d_com || !d_chals || !d_left || !d_right || !d_y || !d_pf_incom || !d_pf_partial || !d_pf_enc ||
+      !d_pf_mlwe)
+    return RG_ERR_INVALID;
+  if (batch < 1 || (batch > 1 && (!d_bq || !d_bo))) return RG_ERR_INVALID;
+  RG_TRY(on_device(J));
+  const rg_jindo_params& p = J->p;
+  const int d = p.d, nq = p.nq, nqo = p.nqo, L = p.field_limbs;
+  const long long pq = (long long)nq * d, po = (long long)nqo * d, nm = p.in_msis + p.mlwe;
+  hipStream_t st = as_stream(stream);
+  const long long n_out = p.dcmp + p.out_msis, n_in = p.rows + nm + p.in_msis;
+  DevBuf a_out, b_out, c_out, lift, a_in, b_in, c_in, p1, p2, norms, flag, dcd, bd, ev;
+  RG_TRY(a_out.alloc(8 * p.out_msis * po));
+  RG_TRY(b_out.alloc(8 * p.out_msis * po));
+  RG_TRY(c_out.alloc(8 * p.out_msis * po));
+  RG_TRY(lift.alloc(8 * p.dcmp * pq));
+  RG_TRY(a_in.alloc(8 * p.in_msis * pq));
+  RG_TRY(b_in.alloc(8 * p.in_msis * pq));
+  RG_TRY(c_in.alloc(8 * p.in_msis * pq));
+  RG_TRY(p1.alloc(8 * pq));
+  RG_TRY(p2.alloc(8 * pq));
+  RG_TRY(norms.alloc(8 * (n_out + n_in) * kNormW));
+  RG_TRY(flag.alloc(sizeof(int)));
+  RG_TRY(dcd.alloc(8 * (size_t)p.cols * p.slots * L));
+  RG_TRY(bd.alloc(8 * (size_t)batch * L));
+  RG_TRY(ev.alloc(8 * 2 * (size_t)L));
+  uint64_t* nrm = norms.as<uint64_t>();
+  // verifyOuterCommitment (:136-161): A = sum_j com[j][i] * batchOut[j] (or com[0][i]),
+  // C = A * 2^logOutCut - sum_j Out[i][j] * Proof.InCommit[j]
+  if (batch > 1) {
+    MacArgs m = dot_args(J->ro, nqo, d, p.out_msis, (int)batch, d_bo, d_com, pq, (long long)p.out_msis * pq,
+                         a_out.as<uint64_t>());
+    RG_TRY(launch_mac(m, st));
+  } else {
+    RG_HIP(hipMemcpy2DAsync(a_out.p, 8 * po, d_com, 8 * pq, 8 * po, p.out_msis, hipMemcpyDeviceToDevice, st));
+  }
+  {
+    MacArgs m = dot_args(J->ro, nqo, d, 1, p.dcmp, J->ck_out.as<uint64_t>(), d_pf_incom, 0, po, b_out.as<uint64_t>());
+    m.J = p.out_msis;
+    RG_TRY(launch_mac(m, st));
+  }
+  RG_TRY(launch_combine(J->ro, nqo, d, p.log_out_cut, a_out.as<uint64_t>(), b_out.as<uint64_t>(), c_out.as<uint64_t>(),
+                        p.out_msis, st));
+  RG_TRY(launch_norm(J, true, d_pf_incom, p.dcmp, po, nrm, st));
+  RG_TRY(launch_norm(J, true, c_out.as<uint64_t>(), p.out_msis, po, nrm + p.dcmp * kNormW, st));
+  // verifyInnerCommitment (:164-200): lift = MForm(NTT(ModUpQtoP(pfInv.InCommit))) (centred),
+  // A = sum_{j<cols} lift[j in_msis + i] * chals[j] + lift[cols in_msis + i],
+  // C = A * 2^logInCut - (sum In[i][j] * Encode[j] + sum MLWE_ck[i][j] * MLWE[j] + MLWE[mlwe + i])
+  {
+    RoundArgs ra;
+    memset(&ra, 0, sizeof(ra));
+    ra.d = d;
+    ra.cut = 0;
+    ra.src = ring_dev(J->ro, nqo, J->rootso_f, J->rootso_b);
+    ra.dst = ring_dev(J->rq, nq, J->rootsq_f, J->rootsq_b);
+    ra.crt = J->crt_o;
+    ra.dm = J->dst_q;
+    ra.in = d_pf_incom;
+    ra.out = lift.as<uint64_t>();
+    ra.out_stride = pq;
+    ra.out_rows = nq;
+    hipLaunchKernelGGL(round_kernel, dim3((unsigned)p.dcmp), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
+    RG_TRY(check_launch("jindo verify lift"));
+  }
+  {
+    MacArgs m = dot_args(J->rq, nq, d, p.in_msis, p.cols, d_chals, lift.as<uint64_t>(), pq, (long long)p.in_msis * pq,
+                         a_in.as<uint64_t>());
+    m.C = lift.as<uint64_t>() + (long long)p.cols * p.in_msis * pq;
+    m.c_col = pq;
+    RG_TRY(launch_mac(m, st));
+  }
+  {
+    MacArgs m = dot_args(J->rq, nq, d, 1, p.rows, J->ck_in.as<uint64_t>(), d_pf_enc, 0, pq, b_in.as<uint64_t>());
+    m.J = p.in_msis;
+    m.T2 = p.mlwe;
+    m.A2 = J->ck_mlwe.as<uint64_t>();
+    m.B2 = d_pf_mlwe;
+    m.b2_term = pq;
+    m.C = d_pf_mlwe + (long long)p.mlwe * pq;
+    m.c_j = pq;
+    RG_TRY(launch_mac(m, st));
+  }
+  RG_TRY(launch_combine(J->rq, nq, d, p.log_in_cut, a_in.as<uint64_t>(), b_in.as<uint64_t>(), c_in.as<uint64_t>(),
+                        p.in_msis, st));
+  uint64_t* nin = nrm + n_out * kNormW;
+  RG_TRY(launch_norm(J, false, d_pf_enc, p.rows, pq, nin, st));
+  RG_TRY(launch_norm(J, false, d_pf_mlwe, nm, pq, nin + p.rows * kNormW, st));
+  RG_TRY(launch_norm(J, false, c_in.as<uint64_t>(), p.in_msis, pq, nin + (p.rows + nm) * kNormW, st));
+  // verifyConsistency (:203-221): sum left[i] * Encode[i] == sum chals[i] * Partial[i] + PartialMask
+  RG_TRY(launch_mac(dot_args(J->rq, nq, d, 1, p.rows, d_left, d_pf_enc, 0, pq, p1.as<uint64_t>()), st));
+  {
+    MacArgs m = dot_args(J->rq, nq, d, 1, p.cols, d_chals, d_pf_partial, 0, pq, p2.as<uint64_t>());
+    m.C = d_pf_partial + (long long)p.cols * pq;
+    RG_TRY(launch_mac(m, st));
+  }
+  RG_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), st));
+  hipLaunchKernelGGL(neq_kernel, dim3((unsigned)((pq + 255) / 256)), dim3(256), 0, st, p1.as<uint64_t>(),
+                     p2.as<uint64_t>(), pq, flag.as<int>());
+  RG_TRY(check_launch("jindo consistency"));
+  // verifyEval (:224-259): sum_{i,j} right[i slots + j] * Decode(pfInv.Partial[i])[j] ==
+  // sum_i Decode(INTT(IMForm(batch[i])))[0] * y[i]  (or y[0])
+  RG_TRY(decode_any(J, d_pf_partial, p.cols, p.slots, dcd.as<uint64_t>(), st));
+  const uint64_t* yb = d_y;
+  if (batch > 1) {
+    RG_TRY(decode_any(J, d_bq, (long long)batch, 1, bd.as<uint64_t>(), st));
+    yb = bd.as<uint64_t>();
+  }
+  RG_TRY(dot2_any(J, d_right, dcd.as<uint64_t>(), (long long)p.cols * p.slots, yb, d_y, batch > 1 ? (long long)batch : 0,
+                  ev.as<uint64_t>(), st));
+  // results to the host
+  std::vector<uint64_t> hn((size_t)(n_out + n_in) * kNormW), he(2 * L);
+  int hf = 0;
+  RG_HIP(hipMemcpyAsync(hn.data(), nrm, hn.size() * 8, hipMemcpyDeviceToHost, st));
+  RG_HIP(hipMemcpyAsync(he.data(), ev.p, he.size() * 8, hipMemcpyDeviceToHost, st));
+  RG_HIP(hipMemcpyAsync(&hf, flag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  RG_HIP(hipStreamSynchronize(st));
+  memset(res, 0, sizeof(*res));
+  for (long long i = 0; i < n_out; ++i) {
+    uint32_t c = 0;
+    for (int w = 0; w < kNormW; ++w) {
+      const unsigned __int128 t = (unsigned __int128)res->outer_norm_sq[w] + hn[i * kNormW + w] + c;
+      res->outer_norm_sq[w] = (uint64_t)t;
+      c = (uint32_t)(t >> 64);
+    }
+  }
+  for (long long i = n_out; i < n_out + n_in; ++i) {
+    uint32_t c = 0;
+    for (int w = 0; w < kNormW; ++w) {
+      const unsigned __int128 t = (unsigned __int128)res->inner_norm_sq[w] + hn[i * kNormW + w] + c;
+      res->inner_norm_sq[w] = (uint64_t)t;
+      c = (uint32_t)(t >> 64);
+    }
+  }
+  res->outer_ok = norm_below(res->outer_norm_sq, in_com_dcmp_two_nm);
+  res->inner_ok = norm_below(res->inner_norm_sq, res_two_nm);
+  res->consistency_ok = hf == 0;
+  memcpy(res->eval_lhs, he.data(), 8 * L);
+  if (batch > 1) {
+    memcpy(res->eval_rhs, he.data() + L, 8 * L);
+  } else {
+    RG_HIP(hipMemcpy(res->eval_rhs, d_y, 8 * L, hipMemcpyDeviceToHost));
+  }
+  res->eval_ok = memcmp(res->eval_lhs, res->eval_rhs, 8 * L) == 0;
+  res->ok = res->outer_ok && res->inner_ok && res->consistency_ok && res->eval_ok;
+  return RG_OK;
+}
 
 static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** J) {
   if (!out) return RG_ERR_INVALID;

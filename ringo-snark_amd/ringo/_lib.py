@@ -98,6 +98,8 @@ _SIGS = {
     "rg_jindo_eval_partial_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "rg_jindo_eval_reduce_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "rg_jindo_eval_respond_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+    "rg_jindo_verify_dev": (ctypes.c_int, [vp, ctypes.c_size_t] + [vp] * 11 + [ctypes.c_double, ctypes.c_double, vp,
+                                                                            vp]),
     "rg_malloc": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_size_t]),
     "rg_free": (ctypes.c_int, [vp]),
     "rg_memcpy_h2d": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),

@@ -69,6 +69,8 @@ class Parameters:
     qo: list
     field_q: int
     stddevs: tuple = None  # ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe (params.go:99-111)
+    res_two_nm: float = None          # ResTwoNm() (params.go:432-435)
+    in_com_dcmp_two_nm: float = None  # InComDcmpTwoNm() (params.go:437-440)
 
     @classmethod
     def from_dict(cls, P, field_q):
@@ -76,7 +78,8 @@ class Parameters:
                    in_msis=P["in_msis"], out_msis=P["out_msis"], mlwe=P["mlwe"], dcmp=P["in_com_dcmp_len"],
                    log_in_cut=P["log_in_cut"], log_out_cut=P["log_out_cut"], base=P["base"], q=list(P["q"]),
                    qo=list(P["qo"]), field_q=int(field_q),
-                   stddevs=tuple(P[k] for k in STDDEV_KEYS) if all(k in P for k in STDDEV_KEYS) else None)
+                   stddevs=tuple(P[k] for k in STDDEV_KEYS) if all(k in P for k in STDDEV_KEYS) else None,
+                   res_two_nm=P.get("res_two_nm"), in_com_dcmp_two_nm=P.get("in_com_dcmp_two_nm"))
 
     @property
     def L(self):
@@ -289,6 +292,68 @@ class Prover:
         """Proof.Encode and Proof.MLWE (prover.go:300-314)."""
         check(lib().rg_jindo_eval_respond_dev(self.h, _addr(ob_enc), _addr(ob_mlwe), _addr(chals), _addr(pf_enc),
                                               _addr(pf_mlwe), _stream(stream)))
+
+
+class VerifyResultC(ctypes.Structure):  # include/ringo.h rg_jindo_verify_result
+    _fields_ = [("outer_norm_sq", ctypes.c_uint64 * 10), ("inner_norm_sq", ctypes.c_uint64 * 10),
+                ("outer_ok", ctypes.c_int), ("inner_ok", ctypes.c_int), ("consistency_ok", ctypes.c_int),
+                ("eval_ok", ctypes.c_int), ("eval_lhs", ctypes.c_uint64 * 16), ("eval_rhs", ctypes.c_uint64 * 16),
+                ("ok", ctypes.c_int)]
+
+
+@dataclass
+class VerifyResult:
+    ok: bool
+    outer_ok: bool
+    inner_ok: bool
+    consistency_ok: bool
+    eval_ok: bool
+    outer_norm_sq: int
+    inner_norm_sq: int
+    eval_lhs: np.ndarray
+    eval_rhs: np.ndarray
+
+
+class Verifier:
+    """NewVerifier (verifier.go:25-47): the commit key from the CRS and the rings' tables, on the
+    device (the same deterministic state a Prover handle holds)."""
+
+    def __init__(self, params, crs=None, ck=None):
+        self.params = params
+        self._p = Prover(params, crs=crs, ck=ck)
+        self.h = self._p.h
+
+    def verify_dev(self, batch, com, bq, bo, chals, left, right, y, pf_incom, pf_partial, pf_enc, pf_mlwe,
+                   stream=None):
+        """Verify(x, com, y, pf) (verifier.go:50-133) on device buffers, challenges injected
+        (include/ringo.h rg_jindo_verify_dev); bq = bo = None when params.batch == 1."""
+        P = self.params
+        if P.res_two_nm is None or P.in_com_dcmp_two_nm is None:
+            raise RingoPanic("Parameters lack the two-norm bounds")
+        r = VerifyResultC()
+        check(lib().rg_jindo_verify_dev(self.h, batch, _addr(com), _addr(bq), _addr(bo), _addr(chals), _addr(left),
+                                        _addr(right), _addr(y), _addr(pf_incom), _addr(pf_partial), _addr(pf_enc),
+                                        _addr(pf_mlwe), float(P.in_com_dcmp_two_nm), float(P.res_two_nm),
+                                        ctypes.byref(r), _stream(stream)))
+        word = lambda w: sum(int(x) << (64 * i) for i, x in enumerate(w))
+        L = P.L
+        return VerifyResult(bool(r.ok), bool(r.outer_ok), bool(r.inner_ok), bool(r.consistency_ok), bool(r.eval_ok),
+                            word(r.outer_norm_sq), word(r.inner_norm_sq), np.array(r.eval_lhs[:L], np.uint64),
+                            np.array(r.eval_rhs[:L], np.uint64))
+
+    def Verify(self, batch, com, bq, bo, chals, left, right, y, pf_incom, pf_partial, pf_enc, pf_mlwe):
+        """Host arrays (numpy) in the verify_dev layouts: staged to the device, then verify_dev."""
+        import torch
+        if len(com) != batch or len(y) != batch:  # verifier.go:51-54
+            raise RingoPanic("len(v) != params.batch")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+        args = [t(a) for a in (com, bq, bo, chals, left, right, y, pf_incom, pf_partial, pf_enc, pf_mlwe)]
+        return self.verify_dev(batch, *args)
+
+
+def NewVerifier(params, crs):
+    return Verifier(params, crs=crs)
 
 
 def uniform_words_dev(seed, instance, first_word, n, out, stream=None):
