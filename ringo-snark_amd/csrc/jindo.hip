@@ -659,7 +659,8 @@ constexpr int kMac3Tc = 8;  // terms per LDS tile
 struct Mac3Args {
   long long per_col, ncols;
   int J, T1, T2, fold;  // fold: a multiple of kMac3Tc
-  const uint64_t* As;   // [per_col][T1 + T2][JP]
+  int Tp;               // T1 + T2 rounded up to kMac3Tc (the key's zero-padded term count)
+  const uint64_t* As;   // [per_col][Tp][JP]
   const uint64_t* B1;
   long long b1_col, b1_term;
   const uint64_t* B2;
@@ -724,7 +725,7 @@ __global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) 
     }
   };
   // key loader role: wave (lkw, jh) stages its own half of lk's slice (8 terms x JW words)
-  const ulonglong2* Aw = reinterpret_cast<const ulonglong2*>(a.As + (long long)lk * T * JP);
+  const ulonglong2* Aw = reinterpret_cast<const ulonglong2*>(a.As + (long long)lk * a.Tp * JP);
   auto aload = [&](int tb, ulonglong2& v) {
     const int tt = lane / (JW / 2), jj = lane % (JW / 2);
     v = (lane < 4 * JW && tb + tt < T) ? Aw[((long long)(tb + tt) * JP + jh * JW) / 2 + jj] : make_ulonglong2(0, 0);
@@ -763,6 +764,9 @@ __global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) 
         Mac3Acc& z = acc[j];
         z.s00 = mad64(a0, b0, z.s00);
         z.s01 = mad64(a0, b1, z.s01);
+        // opaque to reassociation: without it the two middle products are summed first
+        // (mad with 0, mad, 64-bit add = 3 VALU instead of 2 v_mad_u64_u32 into s01)
+        asm("" : "+v"(z.s01));
         z.s01 = mad64(a1, b0, z.s01);
         z.s11 = mad64(a1, b1, z.s11);
       }
@@ -815,6 +819,152 @@ __global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) 
   }
 }
 
+// ---- mac3g: the same products, tiles staged by LDS-DMA (global_load_lds_dwordx4) -----------
+// mac3_kernel runs one workgroup per CU (232 VGPRs, 2 waves/SIMD) with ONE tile in flight,
+// staged through registers: 32 KB of B per CU in flight cannot cover HBM latency, and the MAC
+// waits on memory for ~40% of its cycles.  Here the tiles go HBM -> LDS directly (no VGPR
+// cost), in a ring of kMacRing buffers: while tile i is multiplied, tiles i+1 and i+2 are in
+// flight.  A tile's loads are retired by a counted `s_waitcnt vmcnt` (only the loads issued
+// after it may stay outstanding) and a raw s_barrier (a __syncthreads would drain every DMA).
+// LDS images (lane-linear, as LDS-DMA writes them):
+//   B  [tt][col][8 lk]  one 64-B row per (term, column) = the 8 lk of one HBM row;
+//   A  [lk][tt][JP]     the split key rows of one tile, contiguous per lk in As (padded to Tp).
+// Loads per tile: B = 32 wave-instructions (wave w: term w, four 16-column quarters), A = JP/2
+// (wave w < JP/2: 1 KB of the A image).
+constexpr int kMacRing = 3;
+
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int JP>
+__global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
+  constexpr int NLK = 8;
+  constexpr int BW = kMac3Tc * 64 * NLK;  // B image words per buffer
+  constexpr int AW = NLK * kMac3Tc * JP;  // A image words per buffer
+  constexpr int NA = JP / 2;              // A wave-instructions per tile
+  static_assert(JP * NLK * 64 <= kMacRing * (BW + AW), "output stage must fit the ring");
+  __shared__ uint64_t ring[kMacRing * (BW + AW)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long nlkg = a.per_col / NLK;
+  const long long lk0 = (blockIdx.x % nlkg) * NLK, c0 = (blockIdx.x / nlkg) * 64;
+  const int T = a.T1 + a.T2;
+  const int ntile = a.Tp / kMac3Tc;
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
+  // B loader: wave w stages term w of each tile; quarter k = columns 16k .. 16k+15, lane ->
+  // (column 16k + lane/4, 16-B chunk lane%4 = lk 2(lane%4), +1); clamped addresses past the
+  // last column / term load valid words whose products are discarded (zero key) or unstored
+  const int bq_col = lane >> 2, bq_chunk = lane & 3;
+  auto issue = [&](int tile, int buf) {
+    const uint32_t bbase = ring_lds + (uint32_t)(buf * (BW + AW)) * 8u;
+    int t = tile * kMac3Tc + w;
+    if (t >= T) t = T - 1;
+    const uint64_t* rowbase = t < a.T1 ? a.B1 + (long long)t * a.b1_term : a.B2 + (long long)(t - a.T1) * a.b2_term;
+    const long long colstride = t < a.T1 ? a.b1_col : a.b2_col;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      long long col = c0 + 16 * k + bq_col;
+      if (col >= a.ncols) col = a.ncols - 1;
+      glds16(rowbase + col * colstride + lk0 + 2 * bq_chunk, bbase + (uint32_t)((w * 64 + 16 * k) * NLK) * 8u);
+    }
+    if (w < NA) {  // A image bytes [1024 w, 1024 w + 1024): lane's 16 B = key words (lk, tt, j..j+1)
+      const int u = (w * 64 + lane) * 2;  // u64 index in [lk][tt][JP]
+      const int lk = u / (kMac3Tc * JP), tt = (u / JP) % kMac3Tc, j = u % JP;
+      glds16(a.As + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc + tt) * JP + j,
+             bbase + (uint32_t)(BW + w * 128) * 8u);
+    }
+  };
+  Mac3Acc acc[JP];
+#pragma unroll
+  for (int j = 0; j < JP; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
+  issue(0, 0);
+  if (ntile > 1) issue(1, 1);
+  int since = 0;
+  for (int it = 0; it < ntile; ++it) {
+    const int buf = it % kMacRing;
+    // this wave's loads of tile `it` are done once only tile it+1's (if issued) are outstanding
+    if (it + 1 < ntile) {
+      if (w < NA) wait_vm<5>();
+      else wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's part of tile `it` is in LDS; tile it-1 is consumed
+    if (it + 2 < ntile) issue(it + 2, (it + 2) % kMacRing);
+    const uint64_t* L = ring + buf * (BW + AW) + lane * NLK + w;
+    const uint64_t* LA = ring + buf * (BW + AW) + BW + w * (kMac3Tc * JP);
+#pragma unroll
+    for (int tt = 0; tt < kMac3Tc; ++tt) {
+      const uint64_t b = L[tt * 64 * NLK];
+      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29);
+#pragma unroll
+      for (int j = 0; j < JP; ++j) {
+        const uint64_t av = LA[tt * JP + j];
+        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32);
+        Mac3Acc& z = acc[j];
+        z.s00 = mad64(a0, b0, z.s00);
+        z.s01 = mad64(a0, b1, z.s01);
+        asm("" : "+v"(z.s01));
+        z.s01 = mad64(a1, b0, z.s01);
+        z.s11 = mad64(a1, b1, z.s11);
+      }
+    }
+    since += kMac3Tc;
+    if (since >= a.fold) {
+#pragma unroll
+      for (int j = 0; j < JP; ++j) mac3_fold(acc[j]);
+      since = 0;
+    }
+  }
+  __syncthreads();  // every DMA retired (vmcnt(0) above) and every wave done with the ring
+  const int lk = (int)lk0 + w;
+  const RnsPrime& P = a.P[lk / a.d];
+  const uint64_t q = P.q;
+#pragma unroll
+  for (int j = 0; j < JP; ++j) {
+    mac3_fold(acc[j]);
+    uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
+    r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
+    ring[(j * NLK + w) * 64 + lane] = r;  // [j][lk][col]
+  }
+  __syncthreads();
+  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // 8 lk never straddle a limb (d % 8 == 0)
+  for (int pidx = tid; pidx < JP * 64; pidx += 512) {
+    const int c = pidx & 63, j = pidx >> 6;
+    const long long col = c0 + c;
+    if (j >= a.J || col >= a.ncols) continue;
+    uint64_t r[NLK];
+#pragma unroll
+    for (int x = 0; x < NLK; ++x) r[x] = ring[(j * NLK + x) * 64 + c];
+    if (a.C) {
+      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
+#pragma unroll
+      for (int i = 0; i < NLK / 2; ++i) {
+        const ulonglong2 cv = cp[i];
+        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
+        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
+      }
+    }
+    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
+#pragma unroll
+    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
+  }
+}
+
 // J padded to the instantiated widths
 static int mac3_jp(int J) {
   static const int w[] = {4, 6, 8, 10, 12, 16};
@@ -848,6 +998,22 @@ static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
   const int jp = mac3_jp(m.J);
   const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
   const dim3 g((unsigned)blocks), b(512);
+  static int regstage = -1;  // RINGO_MAC3=r: the register-staged mac3_kernel (comparison runs)
+  if (regstage < 0) {
+    const char* e = getenv("RINGO_MAC3");
+    regstage = (e && e[0] == 'r') ? 1 : 0;
+  }
+  if (!regstage) {
+    switch (jp) {
+      case 4: hipLaunchKernelGGL((mac3g_kernel<4>), g, b, 0, st, m); break;
+      case 6: hipLaunchKernelGGL((mac3g_kernel<6>), g, b, 0, st, m); break;
+      case 8: hipLaunchKernelGGL((mac3g_kernel<8>), g, b, 0, st, m); break;
+      case 10: hipLaunchKernelGGL((mac3g_kernel<10>), g, b, 0, st, m); break;
+      case 12: hipLaunchKernelGGL((mac3g_kernel<12>), g, b, 0, st, m); break;
+      default: hipLaunchKernelGGL((mac3g_kernel<16>), g, b, 0, st, m); break;
+    }
+    return check_launch("jindo mac3g");
+  }
   switch (jp) {
     case 4: hipLaunchKernelGGL((mac3_kernel<4, 1>), g, b, 0, st, m); break;
     case 6: hipLaunchKernelGGL((mac3_kernel<6, 1>), g, b, 0, st, m); break;
@@ -860,24 +1026,26 @@ static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
 }
 
 // the commit key of one MAC, split and transposed for mac3_kernel (on the device):
-// out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J zero)
+// out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J and terms
+// t >= T1 + T2, up to the padded count Tp, zero)
 __global__ __launch_bounds__(256) void mac3_key_kernel(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J,
                                                        int JP, long long per_col, uint64_t* out) {
-  const int T = T1 + T2;
+  const int T = T1 + T2, Tp = (T + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= per_col * T * JP) return;
+  if (i >= per_col * Tp * JP) return;
   const int j = (int)(i % JP);
-  const int t = (int)((i / JP) % T);
-  const long long lk = i / ((long long)JP * T);
+  const int t = (int)((i / JP) % Tp);
+  const long long lk = i / ((long long)JP * Tp);
   uint64_t x = 0;
-  if (j < J) x = t < T1 ? A1[((long long)j * T1 + t) * per_col + lk] : A2[((long long)j * T2 + (t - T1)) * per_col + lk];
+  if (j < J && t < T) x = t < T1 ? A1[((long long)j * T1 + t) * per_col + lk] : A2[((long long)j * T2 + (t - T1)) * per_col + lk];
   out[i] = (x & 0x1fffffffull) | ((x >> 29) << 32);
 }
 
 static rg_status mac3_key_dev(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J, size_t per_col, DevBuf& out,
                               hipStream_t st) {
   const int JP = mac3_jp(J);
-  const long long n = (long long)per_col * (T1 + T2) * JP;
+  const int Tp = (T1 + T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
+  const long long n = (long long)per_col * Tp * JP;
   RG_TRY(out.alloc((size_t)n * 8));
   hipLaunchKernelGGL(mac3_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A1, T1, A2, T2, J, JP,
                      (long long)per_col, out.as<uint64_t>());
@@ -2422,6 +2590,7 @@ static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
   a.T1 = m.T1;
   a.T2 = m.T2;
   a.fold = fold;
+  a.Tp = (m.T1 + m.T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
   a.As = As;
   a.B1 = m.B1;
   a.b1_col = m.b1_col;
