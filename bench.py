@@ -401,6 +401,50 @@ def polyops_bench(torch, ringo, q, L, rank, batch, steps, seed):
         ms = ev.total_ms() / steps
         res[name] = {"ms": ms, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9}
     res["shape"] = "N=2^16, q255 (L=4); aut/quorem over %d polys, evaluate of one" % batch
+    res["buckler"] = buckler_bench(torch, ringo, F, q, L, rank, batch, steps, seed)
+    return res
+
+
+def buckler_bench(torch, ringo, F, q, L, emb, batch, steps, seed):
+    """The Buckler prover's per-witness device work at embRank = N (q255): RandEncode of `batch`
+    witnesses of rank N/2 (buckler/encoder.go:50-54: batched cyclic InvNTT + embedding; bytes =
+    read rank + write embRank elements per witness) and the fused evalCircuit of one constraint
+    a*b - c + pw*d over 4 witnesses + 1 public witness (prover.go:355-379; bytes = 5 polys read +
+    1 written)."""
+    from ringo import buckler
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rank = emb // 2
+    enc = buckler.NewEncoder(F, rank, emb)
+    v = torch.from_numpy(uniform_elems(q, L, batch * rank, seed + 1).view(np.int64).reshape(-1)).to(dev)
+    r = torch.from_numpy(uniform_elems(q, L, batch, seed + 2).view(np.int64).reshape(-1)).to(dev)
+    out = torch.empty(batch * emb * L, dtype=torch.int64, device=dev)
+    scr = torch.empty(max(1, enc.scratch_bytes(batch) // 8), dtype=torch.int64, device=dev)
+    c = buckler.ArithmeticConstraint(F)
+    c.AddTerm(None, 0, 1)
+    c.SubTerm(None, 2)
+    c.AddTerm(0, 3)
+    circ = buckler.Circuit(F, [c])
+    w = torch.from_numpy(uniform_elems(q, L, 4 * emb, seed + 3).view(np.int64).reshape(-1)).to(dev)
+    pw = torch.from_numpy(uniform_elems(q, L, emb, seed + 4).view(np.int64).reshape(-1)).to(dev)
+    bc = w[:L].clone()
+    eo = torch.empty(emb * L, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream()
+    res = {}
+    for name, fn, nbytes in (
+            ("rand_encode", lambda: enc.encode_dev(out, v, batch, d_rand=r, d_scratch=scr, stream=st),
+             8 * L * (rank + emb) * batch),
+            ("eval_circuit", lambda: circ.eval_dev(emb, bc, w, 4, pw, 1, eo, stream=st), 6 * 8 * L * emb)):
+        fn()
+        torch.cuda.synchronize()
+        ev = Events(torch, st)
+        ev.start()
+        for _ in range(steps):
+            fn()
+        ev.stop()
+        torch.cuda.synchronize()
+        ms = ev.total_ms() / steps
+        res[name] = {"ms": ms, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9}
+    res["shape"] = "q255 (L=4), embRank 2^16: RandEncode of %d rank-2^15 witnesses; evalCircuit a*b - c + pw*d" % batch
     return res
 
 

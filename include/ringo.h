@@ -134,6 +134,38 @@ rg_status rg_poly_evaluate_dev(const rg_field* f, const uint64_t* d_p, size_t n,
 size_t rg_poly_evaluate_scratch_bytes(const rg_field* f, size_t n);
 rg_status rg_poly_evaluate(const rg_field* f, const uint64_t* p, size_t n, const uint64_t* x, uint64_t* out);
 
+/* ---- Buckler prover device work -------------------------------- */
+/* Encoder.EncodeTo / RandEncodeTo (buckler/encoder.go:32-54) of `batch` witness vectors:
+ * t is the encoder's CyclicTransformer at the witness rank (newEncoder, encoder.go:15-20; a
+ * negacyclic plan is RG_ERR_INVALID).  d_v [batch][rank][L] -> d_out [batch][embed_rank][L]:
+ * InvNTT into coefficients 0..rank-1, zeros above.  d_rand [batch][L] (NULL = EncodeTo) holds
+ * RandEncodeTo's MustSetRandom draws (Montgomery, injected): coeff[rank] = r, coeff[0] -= r.
+ * batch > 1 needs d_scratch of rg_buckler_encode_scratch_bytes(t, batch) bytes. */
+rg_status rg_buckler_encode_dev(const rg_ntt* t, size_t embed_rank, uint64_t* d_out, const uint64_t* d_v,
+                                size_t batch, const uint64_t* d_rand, uint64_t* d_scratch, void* stream);
+size_t rg_buckler_encode_scratch_bytes(const rg_ntt* t, size_t batch);
+rg_status rg_buckler_encode(const rg_ntt* t, size_t embed_rank, uint64_t* out, const uint64_t* v,
+                            const uint64_t* rand);
+/* The arithmetic constraints Prover.evalCircuit walks (buckler/constraint.go:6-12, built by
+ * AddTerm / SubTerm / AddTermWithConst): constraint c owns terms term_off[c] .. term_off[c+1]-1;
+ * term t = coeffs[t] ([L], Montgomery, < q) * public witness pw_idx[t] (< 0: none, the
+ * hasCoeffPublicWitness flag) * witnesses wit_idx[wit_off[t] .. wit_off[t+1]-1] (witnessToID
+ * numbering).  Uploaded once (Compile time); immutable. */
+typedef struct rg_circuit rg_circuit;
+rg_status rg_buckler_circuit_create(const rg_field* f, size_t n_constraints, const size_t* term_off,
+                                    const uint64_t* coeffs, const long long* pw_idx, const size_t* wit_off,
+                                    const uint64_t* wit_idx, rg_circuit** out);
+void rg_buckler_circuit_destroy(rg_circuit* c);
+/* Prover.evalCircuit(batchConst, constraints, wData) (buckler/prover.go:355-379): d_out [rank][L]
+ * = sum_c batchConst * sum_t coeff_t * pwEcdNTT[pw_t] * prod wEcdNTT[w], NTT domain, fused in one
+ * pass.  d_w [n_w][rank][L] = wEcdNTT, d_pw [n_pw][rank][L] = pwEcdNTT, d_batch_const one element;
+ * a witness index >= n_w (n_pw) is RG_ERR_INVALID. */
+rg_status rg_buckler_eval_circuit_dev(const rg_circuit* c, size_t rank, const uint64_t* d_batch_const,
+                                      const uint64_t* d_w, size_t n_w, const uint64_t* d_pw, size_t n_pw,
+                                      uint64_t* d_out, void* stream);
+rg_status rg_buckler_eval_circuit(const rg_circuit* c, size_t rank, const uint64_t* batch_const, const uint64_t* w,
+                                  size_t n_w, const uint64_t* pw, size_t n_pw, uint64_t* out);
+
 /* ------------------------------------------------------------------------------------ */
 /* Jindo commitment (jindo/params.go, encoder.go, rns.go, prover.go, entities.go)         */
 /* ------------------------------------------------------------------------------------ */

@@ -35,6 +35,10 @@ def lib():
         L.of_quorem_vanishing.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, u64p, u64p, u64p]
         L.of_aut.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_int, u64p, u64p]
         L.of_poly_evaluate.argtypes = [ctypes.c_void_p, u64p, ctypes.c_long, u64p, u64p]
+        L.of_buckler_encode.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_int, ctypes.c_long, u64p, u64p, u64p]
+        lp = ctypes.POINTER(ctypes.c_long)
+        L.of_buckler_eval_circuit.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, lp, u64p, lp, lp, lp,
+                                              u64p, u64p, u64p, u64p]
         L.of_jindo_eval_batch.argtypes = [ctypes.c_void_p, ctypes.c_long] + [u64p] * 8
         L.of_jindo_eval_partial.argtypes = [ctypes.c_void_p, u64p, u64p, u64p]
         L.of_jindo_eval_respond.argtypes = [ctypes.c_void_p] + [u64p] * 5
@@ -131,6 +135,42 @@ class CField:
         xx = np.ascontiguousarray(x, np.uint64).reshape(self.L)
         out = np.zeros(self.L, np.uint64)
         lib().of_poly_evaluate(self.buf, ptr(p), p.shape[0], ptr(xx), ptr(out))
+        return out
+
+    # ---- buckler prover (buckler/encoder.go:32-54, buckler/prover.go:355-379) ----
+    def buckler_encode(self, v, emb, rnd=None):
+        """Encoder.EncodeTo / RandEncodeTo of v [rank, L] into a new [emb, L] array."""
+        v = np.ascontiguousarray(v, np.uint64)
+        rank = v.shape[0]
+        _, twi, ninv = self.tables(rank, cyclic=True)
+        out = np.zeros((emb, self.L), np.uint64)
+        r = None if rnd is None else np.ascontiguousarray(rnd, np.uint64).reshape(self.L)
+        lib().of_buckler_encode(self.buf, ptr(twi), ptr(ninv), rank, emb, ptr(out), ptr(v), ptr(r))
+        return out
+
+    def buckler_eval_circuit(self, constraints, batch_const, w, pw):
+        """constraints: list of constraints, each a list of terms (coeff [L] Montgomery words,
+        public-witness index or None, [witness indices]); w, pw: [n, rank, L]."""
+        lp = ctypes.POINTER(ctypes.c_long)
+        term_off, coeffs, pw_idx, wit_off, wit_idx = [0], [], [], [0], []
+        for c in constraints:
+            for coeff, p, ws in c:
+                coeffs.append(np.asarray(coeff, np.uint64).reshape(self.L))
+                pw_idx.append(-1 if p is None else p)
+                wit_idx.extend(ws)
+                wit_off.append(len(wit_idx))
+            term_off.append(len(pw_idx))
+        arr = lambda x: np.ascontiguousarray(np.array(x, dtype=np.int64))  # noqa: E731
+        to, pi, wo, wi = arr(term_off), arr(pw_idx), arr(wit_off), arr(wit_idx + [0])
+        cf = np.ascontiguousarray(np.array(coeffs, np.uint64).reshape(-1, self.L)) if coeffs else \
+            np.zeros((1, self.L), np.uint64)
+        w = np.ascontiguousarray(w, np.uint64)
+        rank = w.shape[-2]
+        pwa = np.ascontiguousarray(pw if pw is not None and len(pw) else np.zeros((1, rank, self.L)), np.uint64)
+        out = np.zeros((rank, self.L), np.uint64)
+        bc = np.ascontiguousarray(batch_const, np.uint64).reshape(self.L)
+        lib().of_buckler_eval_circuit(self.buf, rank, len(constraints), ptr(to, lp), ptr(cf), ptr(pi, lp),
+                                      ptr(wo, lp), ptr(wi, lp), ptr(bc), ptr(w), ptr(pwa), ptr(out))
         return out
 
     def tables(self, N, cyclic=False):

@@ -1241,6 +1241,53 @@ void of_poly_evaluate(const of_field* F, const uint64_t* p, long n, const uint64
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* Buckler prover device work, literal restatements                    */
+/* ------------------------------------------------------------------------------------------ */
+/* Encoder.EncodeTo / RandEncodeTo (buckler/encoder.go:32-54): out [emb][L] = cyclic InvNTT of
+ * v [rank][L] (twinv/ninv: the CyclicTransformer's tables at `rank`), zeros above rank; with
+ * rnd (the MustSetRandom draw, Montgomery) coeff[rank] = rnd and coeff[0] -= rnd. */
+void of_buckler_encode(const of_field* F, const uint64_t* twinv, const uint64_t* ninv, int rank, long emb,
+                       uint64_t* out, const uint64_t* v, const uint64_t* rnd) {
+  const int L = F->L;
+  of_ntt_inv(F, out, v, twinv, ninv, rank, 1); /* :33 InvNTTTo(pOut.Coeffs[:rank], v[:rank]) */
+  memset(out + (size_t)rank * L, 0, 8 * (size_t)(emb - rank) * L); /* :34-36 SetUint64(0) */
+  if (rnd) {
+    memcpy(out + (size_t)rank * L, rnd, 8 * (size_t)L); /* :52 Coeffs[rank].MustSetRandom() */
+    f_sub(F, out, out, out + (size_t)rank * L, L);      /* :53 Coeffs[0].Sub(Coeffs[0], Coeffs[rank]) */
+  }
+}
+/* Prover.evalCircuit (buckler/prover.go:355-379), polynomial by polynomial as Go runs it:
+ * constraint c has terms term_off[c] .. term_off[c+1]-1; term t: coeffs[t] ([L]), public
+ * witness pw_idx[t] (< 0: none), witnesses wit_idx[wit_off[t] .. wit_off[t+1]-1].  w [n][rank][L]
+ * and pw [n][rank][L] are the NTT-domain encodings; out [rank][L] (overwritten). */
+void of_buckler_eval_circuit(const of_field* F, long rank, long nc, const long* term_off, const uint64_t* coeffs,
+                             const long* pw_idx, const long* wit_off, const long* wit_idx, const uint64_t* bc,
+                             const uint64_t* w, const uint64_t* pw, uint64_t* out) {
+  const int L = F->L;
+  const size_t n = (size_t)rank * L;
+  uint64_t* eval = (uint64_t*)malloc(8 * n);
+  uint64_t* term = (uint64_t*)malloc(8 * n);
+  memset(out, 0, 8 * n); /* :356 pOut := NewPoly(true) */
+  for (long c = 0; c < nc; ++c) {
+    memset(eval, 0, 8 * n); /* :362 eval.Clear() */
+    for (long t = term_off[c]; t < term_off[c + 1]; ++t) {
+      for (long j = 0; j < rank; ++j) memcpy(term + (size_t)j * L, coeffs + (size_t)t * L, 8 * (size_t)L); /* :363-365 */
+      if (pw_idx[t] >= 0) /* :366-368 MulTo(term, term, pwEcdNTT[..]) */
+        for (long j = 0; j < rank; ++j)
+          f_mul(F, term + (size_t)j * L, term + (size_t)j * L, pw + ((size_t)pw_idx[t] * rank + j) * L, L);
+      for (long k = wit_off[t]; k < wit_off[t + 1]; ++k) /* :369-371 MulTo(term, term, wEcdNTT[..]) */
+        for (long j = 0; j < rank; ++j)
+          f_mul(F, term + (size_t)j * L, term + (size_t)j * L, w + ((size_t)wit_idx[k] * rank + j) * L, L);
+      for (long j = 0; j < rank; ++j) f_add(F, eval + (size_t)j * L, eval + (size_t)j * L, term + (size_t)j * L, L); /* :372 */
+    }
+    for (long j = 0; j < rank; ++j) f_mul(F, eval + (size_t)j * L, eval + (size_t)j * L, bc, L); /* :374 ScalarMulTo */
+    for (long j = 0; j < rank; ++j) f_add(F, out + (size_t)j * L, out + (size_t)j * L, eval + (size_t)j * L, L); /* :375 */
+  }
+  free(eval);
+  free(term);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Samplers (math/csprng) and the randomness Prover.Commit draws (prover.go:65-139,           */
 /* encoder.go:149-183), restated from the Go source over OpenSSL's AES (loaded at run time)    */
 /* with the library's instance layout (include/ringo.h rg_jindo_seeds): instance n of a domain */

@@ -249,6 +249,9 @@ static rg_ntt* new_plan(const rg_field* f, int rank, int negacyclic) {
   return t;
 }
 
+const rg_field* ntt_field(const rg_ntt* t) { return &t->f; }
+bool ntt_negacyclic(const rg_ntt* t) { return t->negacyclic != 0; }
+
 }  // namespace rg
 
 using namespace rg;
@@ -298,6 +301,7 @@ rg_status rg_ntt_create_from_tables(const rg_field* f, int rank, int negacyclic,
 
 void rg_ntt_destroy(rg_ntt* t) { delete t; }
 int rg_ntt_rank(const rg_ntt* t) { return t ? t->N : 0; }
+
 
 rg_status rg_ntt_tables(const rg_ntt* t, uint64_t* tw, uint64_t* tw_inv, uint64_t* rank_inv) {
   if (!t) return RG_ERR_INVALID;

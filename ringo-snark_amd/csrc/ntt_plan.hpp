@@ -26,6 +26,10 @@ struct NttLaunch {
   size_t batch;
 };
 
+// the field and kind of a plan (for the operators built on it: buckler.hip)
+const rg_field* ntt_field(const rg_ntt* t);
+bool ntt_negacyclic(const rg_ntt* t);
+
 rg_status ntt_run_L1(const NttLaunch& p, hipStream_t st);
 // lazy single-word pass kernels (ntt_l1_lazy.hip); sets *handled when the shape is covered
 rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled);

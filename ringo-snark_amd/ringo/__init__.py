@@ -14,4 +14,4 @@ from ._lib import RingoError, lib  # noqa: F401
 from .bigpoly import (CyclicTransformer, CyclotomicTransformer, Field, NewCyclicEvaluator,  # noqa: F401
                       NewCyclicTransformer, NewCyclotomicEvaluator, NewCyclotomicTransformer, Poly,
                       RingoPanic)
-from . import jindo  # noqa: F401
+from . import buckler, jindo  # noqa: F401

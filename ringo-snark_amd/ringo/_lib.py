@@ -72,6 +72,17 @@ _SIGS = {
     "rg_poly_evaluate_dev": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, vp, vp]),
     "rg_poly_evaluate_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
     "rg_poly_evaluate": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u64p, u64p]),
+    "rg_buckler_encode_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp, vp]),
+    "rg_buckler_encode_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
+    "rg_buckler_encode": (ctypes.c_int, [vp, ctypes.c_size_t, u64p, u64p, u64p]),
+    "rg_buckler_circuit_create": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), u64p,
+                                                 ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_size_t),
+                                                 u64p, ctypes.POINTER(vp)]),
+    "rg_buckler_circuit_destroy": (None, [vp]),
+    "rg_buckler_eval_circuit_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t,
+                                                   vp, vp]),
+    "rg_buckler_eval_circuit": (ctypes.c_int, [vp, ctypes.c_size_t, u64p, u64p, ctypes.c_size_t, u64p,
+                                               ctypes.c_size_t, u64p]),
     "rg_jindo_create": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), u64p, u64p, u64p, ctypes.POINTER(vp)]),
     "rg_jindo_create_from_crs": (ctypes.c_int, [ctypes.POINTER(JindoParamsC), ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.POINTER(vp)]),
