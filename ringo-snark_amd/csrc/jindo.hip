@@ -661,6 +661,7 @@ struct Mac3Args {
   int J, T1, T2, fold;  // fold: a multiple of kMac3Tc
   int Tp;               // T1 + T2 rounded up to kMac3Tc (the key's zero-padded term count)
   const uint64_t* As;   // [per_col][Tp][JP]
+  const uint32_t* Ss;   // [per_col][Tp][JP]  a0 + a1 of the same key words (mac3g's Karatsuba middle)
   const uint64_t* B1;
   long long b1_col, b1_term;
   const uint64_t* B2;
@@ -681,6 +682,13 @@ __device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
   a.lo = addc(a.lo, a.s11 << 58, c2);
   a.hi += (a.s01 >> 35) + (a.s11 >> 6) + c0 + c1 + c2;
   a.s00 = a.s01 = a.s11 = 0;
+}
+
+// Karatsuba accumulators of mac3g: sm = sum (a0 + a1)(b0 + b1), so the middle sum is
+// s01 = sm - s00 - s11 (exact: sm holds every product of the four); folded like Mac3Acc
+__device__ __forceinline__ void mac3k_fold(Mac3Acc& a) {
+  a.s01 -= a.s00 + a.s11;
+  mac3_fold(a);
 }
 
 // JS = 2 would split the JP outputs of a (column, lk) across two waves (JP / 2 accumulators each,
@@ -856,8 +864,11 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
   constexpr int BW = kMac3Tc * 64 * NLK;  // B image words per buffer
   constexpr int AW = NLK * kMac3Tc * JP;  // A image words per buffer
   constexpr int NA = JP / 2;              // A wave-instructions per tile
-  static_assert(JP * NLK * 64 <= kMacRing * (BW + AW), "output stage must fit the ring");
-  __shared__ uint64_t ring[kMacRing * (BW + AW)];
+  constexpr int SW = NLK * kMac3Tc * JP / 2;  // S image (u32 a0 + a1) words per buffer
+  constexpr int NS = (JP + 3) / 4;            // S wave-instructions per tile (16 JP 16-B chunks)
+  constexpr int RW = BW + AW + SW;            // ring words per buffer
+  static_assert(JP * NLK * 64 <= kMacRing * RW, "output stage must fit the ring");
+  __shared__ uint64_t ring[kMacRing * RW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long nlkg = a.per_col / NLK;
@@ -870,7 +881,7 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
   // last column / term load valid words whose products are discarded (zero key) or unstored
   const int bq_col = lane >> 2, bq_chunk = lane & 3;
   auto issue = [&](int tile, int buf) {
-    const uint32_t bbase = ring_lds + (uint32_t)(buf * (BW + AW)) * 8u;
+    const uint32_t bbase = ring_lds + (uint32_t)(buf * RW) * 8u;
     int t = tile * kMac3Tc + w;
     if (t >= T) t = T - 1;
     const uint64_t* rowbase = t < a.T1 ? a.B1 + (long long)t * a.b1_term : a.B2 + (long long)(t - a.T1) * a.b2_term;
@@ -887,6 +898,15 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
       glds16(a.As + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc + tt) * JP + j,
              bbase + (uint32_t)(BW + w * 128) * 8u);
     }
+    if (w < NS) {  // S image bytes [1024 w, ...): lane's 16 B = four u32 sums (lk, tt, j..j+3)
+      const int c = w * 64 + lane;
+      if (c < 16 * JP) {
+        const int u = 4 * c;  // u32 index in [lk][tt][JP]
+        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
+        glds16(a.Ss + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r,
+               bbase + (uint32_t)(BW + AW) * 8u + (uint32_t)w * 1024u);  // lane-linear: + 16 lane
+      }
+    }
   };
   Mac3Acc acc[JP];
 #pragma unroll
@@ -898,35 +918,35 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
     const int buf = it % kMacRing;
     // this wave's loads of tile `it` are done once only tile it+1's (if issued) are outstanding
     if (it + 1 < ntile) {
-      if (w < NA) wait_vm<5>();
+      if (w < NS) wait_vm<6>();
+      else if (w < NA) wait_vm<5>();
       else wait_vm<4>();
     } else {
       wait_vm<0>();
     }
     __builtin_amdgcn_s_barrier();  // every wave's part of tile `it` is in LDS; tile it-1 is consumed
     if (it + 2 < ntile) issue(it + 2, (it + 2) % kMacRing);
-    const uint64_t* L = ring + buf * (BW + AW) + lane * NLK + w;
-    const uint64_t* LA = ring + buf * (BW + AW) + BW + w * (kMac3Tc * JP);
+    const uint64_t* L = ring + buf * RW + lane * NLK + w;
+    const uint64_t* LA = ring + buf * RW + BW + w * (kMac3Tc * JP);
+    const uint32_t* LS = reinterpret_cast<const uint32_t*>(ring + buf * RW + BW + AW) + w * (kMac3Tc * JP);
 #pragma unroll
     for (int tt = 0; tt < kMac3Tc; ++tt) {
       const uint64_t b = L[tt * 64 * NLK];
-      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29);
+      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29), bs = b0 + b1;
 #pragma unroll
       for (int j = 0; j < JP; ++j) {
         const uint64_t av = LA[tt * JP + j];
-        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32);
-        Mac3Acc& z = acc[j];
+        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32), as = LS[tt * JP + j];
+        Mac3Acc& z = acc[j];  // Karatsuba: 3 v_mad_u64_u32 per MAC (s01 holds sm until the fold)
         z.s00 = mad64(a0, b0, z.s00);
-        z.s01 = mad64(a0, b1, z.s01);
-        asm("" : "+v"(z.s01));
-        z.s01 = mad64(a1, b0, z.s01);
+        z.s01 = mad64(as, bs, z.s01);
         z.s11 = mad64(a1, b1, z.s11);
       }
     }
     since += kMac3Tc;
     if (since >= a.fold) {
 #pragma unroll
-      for (int j = 0; j < JP; ++j) mac3_fold(acc[j]);
+      for (int j = 0; j < JP; ++j) mac3k_fold(acc[j]);
       since = 0;
     }
   }
@@ -936,7 +956,7 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
   const uint64_t q = P.q;
 #pragma unroll
   for (int j = 0; j < JP; ++j) {
-    mac3_fold(acc[j]);
+    mac3k_fold(acc[j]);
     uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
     r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
     ring[(j * NLK + w) * 64 + lane] = r;  // [j][lk][col]
@@ -950,6 +970,163 @@ __global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
     uint64_t r[NLK];
 #pragma unroll
     for (int x = 0; x < NLK; ++x) r[x] = ring[(j * NLK + x) * 64 + c];
+    if (a.C) {
+      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
+#pragma unroll
+      for (int i = 0; i < NLK / 2; ++i) {
+        const ulonglong2 cv = cp[i];
+        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
+        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
+      }
+    }
+    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
+#pragma unroll
+    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
+  }
+}
+
+// ---- mac3h: two columns per lane, half the outputs per wave ----------------------------------
+// mac3g is LDS-bound, not VALU-bound: every MAC needs its key words as a wave-uniform LDS read
+// (12 B: a0 | a1 and a0 + a1), and a uniform ds_read_b128 still costs the LDS 4 cycles, so the
+// key reads of 8 waves alone (3,072 LDS cycles per tile) outrun a SIMD's multiplies (~3,456);
+// its B reads (lane stride 64 B) are 8-way bank conflicts on top.  Here a lane owns TWO
+// columns (c, c + 64) and a wave HALF the outputs (JP / 2) of one lk, so each broadcast key word
+// feeds two columns: key LDS cycles per MAC halve at the same 160 accumulator VGPRs.  B goes
+// to LDS as [tt][2-lk chunk m][128 columns][2 lk] (one LDS-DMA = one chunk of 64 columns), so a
+// lane's b64 read has a 16-B lane stride: 2-way, not 8-way.  Workgroup = 128 columns x 4 lk;
+// blocks are mapped XCD-major so the 4 lk groups sharing a 128-B line of B run on one XCD.
+template <int JP, int JG>
+__global__ __launch_bounds__(256 * JG, 1) void mac3h_kernel(Mac3Args a) {
+  constexpr int NLK = 4, JH = JP / JG, NC = 128, NW = 4 * JG;  // JG output groups: NW waves
+  constexpr int BW = kMac3Tc * 2 * NC * 2;  // B image words per buffer: [tt][m][col][2]
+  constexpr int AW = NLK * kMac3Tc * JP;    // A image words: [lk][tt][JP]
+  constexpr int SW = NLK * kMac3Tc * JP / 2;  // S image words (u32 sums): [lk][tt][JP]
+  constexpr int NA = (JP + 3) / 4;          // A wave-instructions per tile (16 JP chunks of 16 B)
+  constexpr int NS = (JP + 7) / 8;          // S wave-instructions per tile (8 JP chunks)
+  constexpr int RW = BW + AW + SW;
+  static_assert(JP * NLK * NC <= kMacRing * RW, "output stage must fit the ring");
+  static_assert(JP % JG == 0 && (JG == 2 || JG == 4), "output groups");
+  constexpr int BPW = 32 / NW;  // B wave-instructions per wave per tile (32 per tile)
+  __shared__ uint64_t ring[kMacRing * RW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lkw = w & 3, jh = w >> 2;
+  static_assert(NS <= NA, "wait counts");
+  unsigned g = blockIdx.x;
+  if ((gridDim.x & 7) == 0) g = (g & 7) * (gridDim.x >> 3) + (g >> 3);  // XCD-major
+  const long long nlkg = a.per_col / NLK;
+  const long long lk0 = (long long)(g % nlkg) * NLK, c0 = (long long)(g / nlkg) * NC;
+  const int T = a.T1 + a.T2;
+  const int ntile = a.Tp / kMac3Tc;
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
+  auto issue = [&](int tile, int buf) {
+    const uint32_t bbase = ring_lds + (uint32_t)(buf * RW) * 8u;
+    // B: 32 instructions (tt, m, column half h) per tile, BPW per wave
+#pragma unroll
+    for (int k = 0; k < BPW; ++k) {
+      const int idx = w * BPW + k, tt = idx >> 2, m = (idx >> 1) & 1, h = idx & 1;
+      int t = tile * kMac3Tc + tt;
+      if (t >= T) t = T - 1;  // clamped: the key's padded terms are zero
+      const uint64_t* rowbase = t < a.T1 ? a.B1 + (long long)t * a.b1_term : a.B2 + (long long)(t - a.T1) * a.b2_term;
+      const long long colstride = t < a.T1 ? a.b1_col : a.b2_col;
+      long long col = c0 + h * 64 + lane;
+      if (col >= a.ncols) col = a.ncols - 1;
+      glds16(rowbase + col * colstride + lk0 + 2 * m, bbase + (uint32_t)(((tt * 2 + m) * NC + h * 64) * 2) * 8u);
+    }
+    if (w < NA) {  // A: lane's 16 B = key words (lk, tt, j..j+1)
+      const int c = w * 64 + lane;
+      if (c < 16 * JP) {
+        const int u = 2 * c;
+        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
+        glds16(a.As + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r, bbase + (uint32_t)(BW + w * 128) * 8u);
+      }
+    }
+    if (w < NS) {  // S: lane's 16 B = four u32 sums (lk, tt, j..j+3)
+      const int c = w * 64 + lane;
+      if (c < 8 * JP) {
+        const int u = 4 * c;
+        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
+        glds16(a.Ss + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r,
+               bbase + (uint32_t)(BW + AW) * 8u + (uint32_t)w * 1024u);
+      }
+    }
+  };
+  Mac3Acc acc[2][JH];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < JH; ++j) acc[h][j] = Mac3Acc{0, 0, 0, 0, 0};
+  issue(0, 0);
+  if (ntile > 1) issue(1, 1);
+  int since = 0;
+  for (int it = 0; it < ntile; ++it) {
+    const int buf = it % kMacRing;
+    if (it + 1 < ntile) {  // only tile it+1's loads may stay outstanding
+      if (w < NS) wait_vm<BPW + 2>();
+      else if (w < NA) wait_vm<BPW + 1>();
+      else wait_vm<BPW>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (it + 2 < ntile) issue(it + 2, (it + 2) % kMacRing);
+    const uint64_t* L = ring + buf * RW + ((lkw >> 1) * NC + lane) * 2 + (lkw & 1);
+    const uint64_t* LA = ring + buf * RW + BW + lkw * (kMac3Tc * JP) + jh * JH;
+    const uint32_t* LS = reinterpret_cast<const uint32_t*>(ring + buf * RW + BW + AW) + lkw * (kMac3Tc * JP) + jh * JH;
+#pragma unroll
+    for (int tt = 0; tt < kMac3Tc; ++tt) {
+      uint32_t b0[2], b1[2], bs[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t b = L[tt * (2 * NC * 2) + h * 128];
+        b0[h] = (uint32_t)b & 0x1fffffffu;
+        b1[h] = (uint32_t)(b >> 29);
+        bs[h] = b0[h] + b1[h];
+      }
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        const uint64_t av = LA[tt * JP + j];
+        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32), as = LS[tt * JP + j];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          Mac3Acc& z = acc[h][j];
+          z.s00 = mad64(a0, b0[h], z.s00);
+          z.s01 = mad64(as, bs[h], z.s01);
+          z.s11 = mad64(a1, b1[h], z.s11);
+        }
+      }
+    }
+    since += kMac3Tc;
+    if (since >= a.fold) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < JH; ++j) mac3k_fold(acc[h][j]);
+      since = 0;
+    }
+  }
+  __syncthreads();
+  const int lk = (int)lk0 + lkw;
+  const RnsPrime& P = a.P[lk / a.d];
+  const uint64_t q = P.q;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < JH; ++j) {
+      mac3k_fold(acc[h][j]);
+      uint64_t r = sh_mul(acc[h][j].lo, P.rinv, P.rinv_sh, q);
+      r = mod_add(r, sh_mul(acc[h][j].hi, 1, P.one_sh, q), q);
+      ring[((jh * JH + j) * NLK + lkw) * NC + h * 64 + lane] = r;  // [j][lk][col]
+    }
+  __syncthreads();
+  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // 4 lk never straddle a limb (d % 8 == 0)
+  for (int pidx = tid; pidx < JP * NC; pidx += 256 * JG) {
+    const int c = pidx & (NC - 1), j = pidx / NC;
+    const long long col = c0 + c;
+    if (j >= a.J || col >= a.ncols) continue;
+    uint64_t r[NLK];
+#pragma unroll
+    for (int x = 0; x < NLK; ++x) r[x] = ring[(j * NLK + x) * NC + c];
     if (a.C) {
       const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
 #pragma unroll
@@ -979,9 +1156,13 @@ static int mac3_jp(int J) {
 static int mac3_fold_period(const RnsPrime* P, int nl) {
   int bits = 29;
   for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
+  // mac3g's Karatsuba middle: (a0 + a1)(b0 + b1) <= smax^2, smax = 2^29 - 1 + max a1 (exact in q)
+  double smax = 0;
+  for (int l = 0; l < nl; ++l) smax = std::max(smax, (double)((1ull << 29) - 1 + ((P[l].q - 1) >> 29)));
   int f = 32;
   while (f > 1 && ((double)f * 2.0 * std::ldexp(1.0, bits) > std::ldexp(1.0, 64) ||
-                   (double)f * std::ldexp(1.0, 2 * std::max(0, bits - 29)) > std::ldexp(1.0, 64)))
+                   (double)f * std::ldexp(1.0, 2 * std::max(0, bits - 29)) > std::ldexp(1.0, 64) ||
+                   (double)f * smax * smax >= std::ldexp(1.0, 64)))
     f >>= 1;
   return f & ~(kMac3Tc - 1);
 }
@@ -998,12 +1179,35 @@ static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
   const int jp = mac3_jp(m.J);
   const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
   const dim3 g((unsigned)blocks), b(512);
-  static int regstage = -1;  // RINGO_MAC3=r: the register-staged mac3_kernel (comparison runs)
+  static int regstage = -1;  // RINGO_MAC3=r / g: mac3_kernel / mac3g_kernel (comparison runs)
   if (regstage < 0) {
     const char* e = getenv("RINGO_MAC3");
-    regstage = (e && e[0] == 'r') ? 1 : 0;
+    regstage = (e && e[0] == 'r') ? 1 : (e && e[0] == 'g') ? 2 : (e && e[0] == '2') ? 3 : 0;  // r: mac3, g: mac3g, 2: mac3h<JP,2>
   }
-  if (!regstage) {
+  if (regstage == 0 || regstage == 3) {  // default: mac3h, 4 output groups where JP allows (3: 2 groups)
+    const dim3 gh((unsigned)((m.ncols + 127) / 128 * (m.per_col / 4)));
+    const dim3 b2(512), b4(1024);
+    const bool g4 = regstage == 0;
+    switch (jp) {
+      case 4: hipLaunchKernelGGL((mac3h_kernel<4, 2>), gh, b2, 0, st, m); break;
+      case 6: hipLaunchKernelGGL((mac3h_kernel<6, 2>), gh, b2, 0, st, m); break;
+      case 8:
+        if (g4) hipLaunchKernelGGL((mac3h_kernel<8, 4>), gh, b4, 0, st, m);
+        else hipLaunchKernelGGL((mac3h_kernel<8, 2>), gh, b2, 0, st, m);
+        break;
+      case 10: hipLaunchKernelGGL((mac3h_kernel<10, 2>), gh, b2, 0, st, m); break;
+      case 12:
+        if (g4) hipLaunchKernelGGL((mac3h_kernel<12, 4>), gh, b4, 0, st, m);
+        else hipLaunchKernelGGL((mac3h_kernel<12, 2>), gh, b2, 0, st, m);
+        break;
+      default:
+        if (g4) hipLaunchKernelGGL((mac3h_kernel<16, 4>), gh, b4, 0, st, m);
+        else hipLaunchKernelGGL((mac3h_kernel<16, 2>), gh, b2, 0, st, m);
+        break;
+    }
+    return check_launch("jindo mac3h");
+  }
+  if (regstage == 2) {
     switch (jp) {
       case 4: hipLaunchKernelGGL((mac3g_kernel<4>), g, b, 0, st, m); break;
       case 6: hipLaunchKernelGGL((mac3g_kernel<6>), g, b, 0, st, m); break;
@@ -1039,6 +1243,7 @@ __global__ __launch_bounds__(256) void mac3_key_kernel(const uint64_t* A1, int T
   uint64_t x = 0;
   if (j < J && t < T) x = t < T1 ? A1[((long long)j * T1 + t) * per_col + lk] : A2[((long long)j * T2 + (t - T1)) * per_col + lk];
   out[i] = (x & 0x1fffffffull) | ((x >> 29) << 32);
+  reinterpret_cast<uint32_t*>(out + per_col * Tp * JP)[i] = (uint32_t)(x & 0x1fffffffull) + (uint32_t)(x >> 29);
 }
 
 static rg_status mac3_key_dev(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J, size_t per_col, DevBuf& out,
@@ -1046,7 +1251,7 @@ static rg_status mac3_key_dev(const uint64_t* A1, int T1, const uint64_t* A2, in
   const int JP = mac3_jp(J);
   const int Tp = (T1 + T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
   const long long n = (long long)per_col * Tp * JP;
-  RG_TRY(out.alloc((size_t)n * 8));
+  RG_TRY(out.alloc((size_t)n * 12 + 16));  // a0 | a1 << 32 words, then the u32 sums a0 + a1
   hipLaunchKernelGGL(mac3_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A1, T1, A2, T2, J, JP,
                      (long long)per_col, out.as<uint64_t>());
   return check_launch("jindo mac3 key");
@@ -2592,6 +2797,7 @@ static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
   a.fold = fold;
   a.Tp = (m.T1 + m.T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
   a.As = As;
+  a.Ss = reinterpret_cast<const uint32_t*>(As + a.per_col * a.Tp * mac3_jp(m.J));
   a.B1 = m.B1;
   a.b1_col = m.b1_col;
   a.b1_term = m.b1_term;
