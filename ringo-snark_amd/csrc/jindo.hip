@@ -376,10 +376,15 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], __amdgpu_buffer_rsr
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
       const rg_u32x4 wv = __builtin_amdgcn_raw_buffer_load_b128(roots, rbase + ((1u << k) + (xof(rho0) >> (b + 1))) * 16u, 0, 0);
       const ulonglong2 w = make_ulonglong2(pk(wv.x, wv.y), pk(wv.z, wv.w));
-      // Harvey: values in [0, 4q) (ring primes are < 2^62), twiddle product in [0, 2q)
+      // Harvey with a 4q-wide twiddle product: values in [0, 8q) (ring primes < 2^61), x
+      // reduced to [0, 4q), t = y w - Q' q in [0, 4q) with Q' the Shoup quotient less the low
+      // cross products (Q - 2 <= Q' <= Q): three 32-bit multiplies for the quotient, not four
       uint64_t x = e[rho0];
-      x = x >= q2 ? x - q2 : x;
-      const uint64_t tt = shoup_mul_lazy(e[rho0 + half], w.x, w.y, q);
+      x = x >= q2 ? x - q2 : x;  // q2 = 4q here
+      const uint64_t y = e[rho0 + half];
+      const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32), p0 = (uint32_t)w.y, p1 = (uint32_t)(w.y >> 32);
+      const uint64_t qa = mad64(y1, p1, __umulhi(y1, p0)) + __umulhi(y0, p1);
+      const uint64_t tt = y * w.x - qa * q;
       e[rho0] = x + tt;
       e[rho0 + half] = x + q2 - tt;
     }
@@ -428,7 +433,7 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     const bool active = limb < nq;
     const int lc = active ? limb : l0;
     const RnsPrime& P = a.R.p[lc];
-    const uint64_t q = P.q, q2 = 2 * q;
+    const uint64_t q = P.q, q2 = 4 * q;  // prep_round's lazy bound: values in [0, 2 q2)
     const __amdgpu_buffer_rsrc_t roots = rg_buf(a.R.fwd);  // uniform; the limb is a lane offset
     const uint32_t rbase = (uint32_t)lc * 256u * 16u;
     // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
@@ -483,9 +488,10 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     prep_round<2, 0, 2>(e, roots, rbase, q, q2, t);
     wave_lds_fence();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {  // [0, 4q) -> [0, q)
+    for (int r = 0; r < 8; ++r) {  // [0, 8q) -> [0, q)
       uint64_t x = e[r];
       x = x >= q2 ? x - q2 : x;
+      x = x >= 2 * q ? x - 2 * q : x;
       lds[rL8 + r] = x >= q ? x - q : x;
     }
     wave_lds_fence();
@@ -2938,7 +2944,9 @@ static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const 
   const long long n_ml = (long long)batch * (p.cols + 1) * nm;
   pa.n_ml = n_ml;
   pa.clim = (long long)(((uint64_t)1 << 61) / p.base);
-  if (d == 256 && !prep_legacy()) {
+  bool q61 = true;  // prep256's lazy [0, 8q) needs q < 2^61 (every configs ring prime is <= 59 bits)
+  for (int l = 0; l < nq; ++l) q61 = q61 && J->rq[l].q < (1ull << 61);
+  if (d == 256 && q61 && !prep_legacy()) {
     static const int pw = [] {  // RINGO_JINDO_PREP_W: minimum waves per SIMD for prep256 (tuning)
       const char* e = getenv("RINGO_JINDO_PREP_W");
       return e ? atoi(e) : 6;
