@@ -315,24 +315,33 @@ def counters():
 
 
 # the kernels of one step of each line (setup kernels and the Evaluate MACs excluded)
-LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("ntt256_pass",),
-                "j14": ("digits_kernel", "prep256_kernel", "mac3_kernel<", "round_kernel"),
-                "j16": ("digits_kernel", "prep256_kernel", "mac3_kernel<", "round_kernel")}
+_DET = ("digits_kernel", "prep256_kernel", "mac3_kernel<", "mac3g_kernel<", "mac3h_kernel<", "round_kernel")
+_SAMP = ("cdt_noise_kernel", "cdt_tail_kernel", "cosac_noise_kernel", "mlwe_noise_kernel", "uniform_elems_kernel")
+LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("ntt256_pass",), "j14": _DET + _SAMP, "j16": _DET + _SAMP}
 
 
 def line_counters(C, line, units_per_step, kernel_ms_per_step):
-    """traffic (HBM bytes per unit) and the VALU issue block for one line, or None."""
+    """traffic (HBM bytes per unit) and the VALU issue block for one line, or None.  A Jindo
+    line's profiled run executes injected steps (the deterministic kernels) and sampled steps
+    (samplers + the same deterministic kernels): each kernel's sums are divided by the steps it
+    ran in, so the figures are per sampled step = per Prover.Commit batch."""
     if C is None or line not in C.get("lines", {}):
         return None, None
     Lc = C["lines"][line]
-    steps = Lc["steps"]
-    ks = [v for n, v in Lc["kernels"].items() if any(p in n for p in LINE_KERNELS[line])]
-    fetch = sum(k.get("FETCH_SIZE", 0.0) for k in ks)  # KiB, summed over dispatches
-    write = sum(k.get("WRITE_SIZE", 0.0) for k in ks)
-    valu = sum(k.get("SQ_INSTS_VALU", 0.0) for k in ks)
-    traffic = (2.0 * fetch + write) * 1024.0 / steps / units_per_step  # gfx950: FETCH_SIZE counts half
-    floor_ms = valu / steps * VALU_CYCLES / (SIMDS * CLOCK_HZ) * 1e3
-    vb = {"insts_per_unit": valu / steps / units_per_step, "cycles_per_inst": VALU_CYCLES, "simds": SIMDS,
+    se = Lc.get("steps_executed") or {line: Lc["steps"]}
+    fetch = write = valu = 0.0
+    for n, k in Lc["kernels"].items():
+        if not any(p in n for p in LINE_KERNELS[line]):
+            continue
+        st = se.get(line, Lc["steps"])
+        if any(p in n for p in _DET):
+            st += se.get(line + "_injected", 0)
+        fetch += k.get("FETCH_SIZE", 0.0) / st  # KiB per step
+        write += k.get("WRITE_SIZE", 0.0) / st
+        valu += k.get("SQ_INSTS_VALU", 0.0) / st
+    traffic = (2.0 * fetch + write) * 1024.0 / units_per_step  # gfx950: FETCH_SIZE counts half
+    floor_ms = valu * VALU_CYCLES / (SIMDS * CLOCK_HZ) * 1e3
+    vb = {"insts_per_unit": valu / units_per_step, "cycles_per_inst": VALU_CYCLES, "simds": SIMDS,
           "clock_ghz": CLOCK_HZ / 1e9, "issue_floor_ms_per_step": floor_ms,
           "frac": floor_ms / kernel_ms_per_step if kernel_ms_per_step else None,
           "note": "SQ_INSTS_VALU (wave64 instructions) x cycles/inst / (SIMDs x clock) = the VALU issue floor; "

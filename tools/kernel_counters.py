@@ -44,6 +44,6 @@ for ldir in sorted(glob.glob(os.path.join(root, "*"))):
     for name, cs in acc.items():
         kern[name] = dict(cs)
         kern[name]["dispatches_per_pass"] = max(v for (f, n), v in calls.items() if n == name)
-    res["lines"][line] = {"steps": steps, "kernels": kern}
+    res["lines"][line] = {"steps": steps, "steps_executed": b["steps_executed"], "kernels": kern}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: {"steps": v["steps"], "kernels": len(v["kernels"])} for k, v in res["lines"].items()}))
