@@ -2123,6 +2123,26 @@ __global__ __launch_bounds__(kCosacThreads) void cosac_noise_kernel(SampleArgs a
     if (!ok) seg[n2 + mb(fm)] = ent;
     n2 += __builtin_popcountll(fm);
   }
+  // ---- phase 2b: the rest again with 7 blocks (<= 6 loop passes), so that the state machine
+  // below, which pays a whole-wave AES block per consumed word, sees ~1/4 of phase 2's rest ----
+  {
+    long long n3 = 0;
+    for (long long i0 = 0; i0 < n2; i0 += 64) {
+      const bool act = i0 + lane < n2;
+      const unsigned long long ent = act ? seg[i0 + lane] : 0;
+      const unsigned long long oi = ent & ((1ull << 62) - 1);
+      bool ok = true;
+      if (act) {
+        long long res = 0;
+        ok = cosac_fast<4, 3>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sds[ent >> 62], Z, res);
+        if (ok) a.enc_noise[oi] = res;
+      }
+      const uint64_t fm = __ballot(!ok);
+      if (!ok) seg[n3 + mb(fm)] = ent;
+      n3 += __builtin_popcountll(fm);
+    }
+    n2 = n3;
+  }
   // ---- phase 3: the state machine over the n2 remaining samples ----
   CosacLane L;
   L.g = -1;
