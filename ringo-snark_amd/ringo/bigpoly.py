@@ -68,10 +68,11 @@ class Field:
         if st != 0:
             raise RingoPanic("invalid modulus")
         self.h = h
+        self._L = lib()
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rg_field_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "_L", None):  # the CDLL bound at creation
+            self._L.rg_field_destroy(self.h)  # (module globals may already be gone at interpreter exit)
             self.h = None
 
     def constants(self):
@@ -131,10 +132,11 @@ class _Transformer:
             raise RingoPanic("NTT not supported")  # ntt.go:35-37,162-164
         check(st)
         self.h = h
+        self._L = lib()
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rg_ntt_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "_L", None):  # the CDLL bound at creation
+            self._L.rg_ntt_destroy(self.h)  # (module globals may already be gone at interpreter exit)
             self.h = None
 
     def Rank(self):

@@ -132,10 +132,11 @@ class Circuit:
             raise RingoPanic("inconsistent input(s)")
         check(st)
         self.h = h
+        self._L = lib()
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rg_buckler_circuit_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "_L", None):  # the CDLL bound at creation
+            self._L.rg_buckler_circuit_destroy(self.h)  # (module globals may already be gone at interpreter exit)
             self.h = None
 
     def eval_dev(self, rank, d_batch_const, d_w, n_w, d_pw, n_pw, d_out, stream=None):

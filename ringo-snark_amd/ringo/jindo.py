@@ -173,13 +173,14 @@ class Prover:
             st = lib().rg_jindo_create_from_crs(ctypes.byref(ps), crs, len(crs), ctypes.byref(h))
         check(st)
         self.h = h
+        self._L = lib()
         if params.stddevs is not None:
             sd = JindoStddevsC(*params.stddevs)
             check(lib().rg_jindo_set_stddevs(self.h, ctypes.byref(sd)))
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rg_jindo_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "_L", None):  # the CDLL bound at creation
+            self._L.rg_jindo_destroy(self.h)  # (module globals may already be gone at interpreter exit)
             self.h = None
 
     def commit_key(self):
