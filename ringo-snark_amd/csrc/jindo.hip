@@ -359,8 +359,8 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("" ::: "memory");
 }
 template <int RK, int LO, int PAT>
-__device__ __forceinline__ void prep_round(uint64_t (&e)[8], __amdgpu_buffer_rsrc_t roots, uint32_t rbase, uint64_t q,
-                                           uint64_t q2, uint32_t t) {
+__device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, uint64_t q, uint64_t q2,
+                                           uint32_t t) {
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
@@ -374,8 +374,7 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], __amdgpu_buffer_rsr
     for (int j = 0; j < 4; ++j) {
       const int grp = j / (NPK / 2), jj = j % (NPK / 2);
       const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1));
-      const rg_u32x4 wv = __builtin_amdgcn_raw_buffer_load_b128(roots, rbase + ((1u << k) + (xof(rho0) >> (b + 1))) * 16u, 0, 0);
-      const ulonglong2 w = make_ulonglong2(pk(wv.x, wv.y), pk(wv.z, wv.w));
+      const ulonglong2 w = roots[(1u << k) + (xof(rho0) >> (b + 1))];  // the limb's table, staged in LDS
       // Harvey with a 4q-wide twiddle product: values in [0, 8q) (ring primes < 2^61), x
       // reduced to [0, 4q), t = y w - Q' q in [0, 4q) with Q' the Shoup quotient less the low
       // cross products (Q - 2 <= Q' <= Q): three 32-bit multiplies for the quotient, not four
@@ -401,8 +400,11 @@ __device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
 template <int MINW>
 __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs a) {
   __shared__ uint64_t lds_all[kPrepWaves][2 * 288];
+  extern __shared__ ulonglong2 tw_lds[];  // the nq limbs' forward tables (w, w'), [nq][256]: dynamic LDS
   const JShape& S = a.s;
   const int nq = S.nq;
+  for (int i = threadIdx.x; i < nq * 256; i += blockDim.x) tw_lds[i] = a.R.fwd[i];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
   const int wv = threadIdx.x >> 6;
   uint64_t* lds = lds_all[wv];
@@ -434,8 +436,7 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     const int lc = active ? limb : l0;
     const RnsPrime& P = a.R.p[lc];
     const uint64_t q = P.q, q2 = 4 * q;  // prep_round's lazy bound: values in [0, 2 q2)
-    const __amdgpu_buffer_rsrc_t roots = rg_buf(a.R.fwd);  // uniform; the limb is a lane offset
-    const uint32_t rbase = (uint32_t)lc * 256u * 16u;
+    const ulonglong2* roots = tw_lds + lc * 256;
     // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
     // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
     // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  Inputs are (re)read per
@@ -472,20 +473,20 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
       }
     }
     // NTT: H round (stages 0-2), H->M, M round (3-5), M->L, L round (6-7), L->H, store
-    prep_round<3, 5, 0>(e, roots, rbase, q, q2, t);
+    prep_round<3, 5, 0>(e, roots, q, q2, t);
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[rM + 4 * y];
-    prep_round<3, 2, 1>(e, roots, rbase, q, q2, t);
+    prep_round<3, 2, 1>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rM + 4 * y + (y >> 1)] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[rL9 + r];
-    prep_round<2, 0, 2>(e, roots, rbase, q, q2, t);
+    prep_round<2, 0, 2>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) {  // [0, 8q) -> [0, q)
@@ -2972,12 +2973,13 @@ static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const 
       return e ? atoi(e) : 6;
     }();
     const dim3 g((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
+    const size_t twl = (size_t)nq * 256 * sizeof(ulonglong2);
     if (pw >= 8)
-      hipLaunchKernelGGL(prep256_kernel<8>, g, b, 0, st, pa);
+      hipLaunchKernelGGL(prep256_kernel<8>, g, b, twl, st, pa);
     else if (pw >= 6)
-      hipLaunchKernelGGL(prep256_kernel<6>, g, b, 0, st, pa);
+      hipLaunchKernelGGL(prep256_kernel<6>, g, b, twl, st, pa);
     else
-      hipLaunchKernelGGL(prep256_kernel<1>, g, b, 0, st, pa);
+      hipLaunchKernelGGL(prep256_kernel<1>, g, b, twl, st, pa);
   } else {
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   }
