@@ -2208,8 +2208,9 @@ __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   aes_lds_fill(lds, a.te0);
   aes_key_fill(key, a.key[kDomMlweRnd]);
   __syncthreads();
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= a.n_ml_pairs) return;
+  // grid-stride: a bounded grid fills the 64 KiB LDS tables once per workgroup, not once per 512 pairs
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.n_ml_pairs;
+       gid += (long long)gridDim.x * blockDim.x) {
   const JShape& S = a.s;
   const int nm = S.in_msis + S.mlwe;
   const int m = (int)(gid % (S.d / 2));
@@ -2229,6 +2230,7 @@ __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
       u.init(key, lds, gpoly * S.d + k);
       out[k] = rounded_gauss(a.zig, u, 0.0, a.sd_mask_mlwe);
     }
+  }
   }
 }
 
@@ -2257,8 +2259,9 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
   aes_lds_fill(lds, a.te0);
   aes_key_fill(key, a.key);
   __syncthreads();
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= a.total) return;
+  // grid-stride (see mlwe_noise_kernel); one draw per iteration
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
+       gid += (long long)gridDim.x * blockDim.x) [&] {
   const JShape& S = a.s;
   const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
   const long long b = gid / per, i = gid % per;
@@ -2268,8 +2271,28 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
     for (int l = 0; l < L; ++l) dst[l] = 0;
     return;
   }
+  const unsigned long long inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
+  if ((L % 2) == 0 && a.kbytes == 8 * L) {  // whole words (e.g. q255: 32 bytes): a try = L/2 blocks, in parallel
+    const uint64_t base = (uint64_t)inst << kWinShift, topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
+    for (uint64_t t = 0;; ++t) {
+      uint64_t z[L];
+      if ((t + 1) * L <= 1024) {
+#pragma unroll
+        for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, base + t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
+      } else {  // past the first 8 KiB buffer (uniform.go:64-82)
+#pragma unroll
+        for (int l = 0; l < L; ++l) z[l] = uniform_word_at(LdsKey{key}, lds, base, t * L + l);
+      }
+      z[L - 1] &= topm;  // the last byte's unused top bits (element.go:320-325)
+      if (!geq_q<L>(z, a.F)) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) dst[l] = z[l];
+        return;
+      }
+    }
+  }
   Uniform u;
-  u.init(key, lds, (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i);
+  u.init(key, lds, inst);
   uint64_t word = 0;
   int left = 0;  // unread bytes of `word`
   for (;;) {
@@ -2295,6 +2318,7 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
       return;
     }
   }
+  }();
 }
 
 // raw Sample() words of one UniformSampler instance (rg_uniform_words_dev)
@@ -3048,7 +3072,8 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.last_row = last;
   a.mask = mask;
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
-  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)((a.total + 511) / 512)), dim3(512), 0, st, a);
+  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)std::min<long long>((a.total + 511) / 512, 1024)), dim3(512),
+                     0, st, a);
   return check_launch("jindo uniform");
 }
 
@@ -3135,7 +3160,8 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 511) / 512)), dim3(512), 0, st, a);
     RG_TRY(check_launch("jindo enc noise"));
   }
-  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)((a.n_ml_pairs + 511) / 512)), dim3(512), 0, st, a);
+  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)std::min<long long>((a.n_ml_pairs + 511) / 512, 1024)), dim3(512),
+                     0, st, a);
   return check_launch("jindo mlwe noise");
 }
 
