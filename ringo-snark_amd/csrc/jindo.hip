@@ -164,6 +164,22 @@ __device__ __forceinline__ uint32_t divstep(uint64_t num, uint64_t b, uint64_t b
   return (uint32_t)qt;
 }
 
+// the same step for a divisor d in (2^31, 2^32) (b^2 of every configs field: 60272^2, 60256^2),
+// whose reciprocal is 2^32 + B0: hi64(num (2^32 + B0)) = r + hi32(r B0 + n0 + hi32(n0 B0)) for
+// num = r 2^32 + n0 -- three 32-bit multiplies instead of a 64 x 64 high product and a 64-bit
+// product
+__device__ __forceinline__ uint32_t divstep_b2(uint32_t r, uint32_t n0, uint32_t d, uint32_t B0, uint32_t& rem) {
+  const uint64_t t = mad64(r, B0, (uint64_t)n0 + __umulhi(n0, B0));
+  uint32_t qt = r + (uint32_t)(t >> 32);
+  uint64_t rm = (((uint64_t)r << 32) | n0) - (uint64_t)qt * d;
+  if (rm >= d) {
+    rm -= d;
+    ++qt;
+  }
+  rem = (uint32_t)rm;
+  return qt;
+}
+
 template <int L>
 __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
   const JShape& S = a.s;
@@ -237,11 +253,20 @@ __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
       return tp;
     };
     int top = top_of();
+    const bool b2fast = (a.b2_inv >> 32) == 1;  // uniform: d in (2^31, 2^32)
     for (; jd + 1 < S.exp - 1; jd += 2) {
       uint64_t rem = 0;
+      if (b2fast) {
+        uint32_t r32 = 0;
 #pragma unroll
-      for (int k = 2 * L - 1; k >= 0; --k)
-        if (k <= top) w[k] = divstep((rem << 32) | w[k], a.b2, a.b2_inv, rem);
+        for (int k = 2 * L - 1; k >= 0; --k)
+          if (k <= top) w[k] = divstep_b2(r32, w[k], (uint32_t)a.b2, (uint32_t)a.b2_inv, r32);
+        rem = r32;
+      } else {
+#pragma unroll
+        for (int k = 2 * L - 1; k >= 0; --k)
+          if (k <= top) w[k] = divstep((rem << 32) | w[k], a.b2, a.b2_inv, rem);
+      }
       top = top_of();
       uint64_t lo;
       const uint32_t hi = divstep(rem, S.base, a.base_inv, lo);
