@@ -284,7 +284,10 @@ rg_status rg_jindo_sample_dev(const rg_jindo* j, size_t batch, const uint64_t* d
                               const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_last_row,
                               uint64_t* d_mask, int64_t* d_enc_noise, int64_t* d_mlwe_noise, void* stream);
 /* Prover.Commit end to end on the device (prover.go:45-202): rg_jindo_sample_dev, then
- * rg_jindo_commit_dev on that randomness (kept in the stream's scratch). */
+ * rg_jindo_commit_dev on that randomness (kept in the stream's scratch).  A batch of >= 64 commits
+ * runs as two halves, one on `stream` and one on a library-owned stream joined to it by events
+ * (the samplers of one half overlap the other half's core); the outputs are complete, as usual,
+ * when `stream` has passed the call. */
 rg_status rg_jindo_commit_sampled_dev(const rg_jindo* j, size_t batch, const uint64_t* d_v, size_t nv,
                                       const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_incom,
                                       uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream);

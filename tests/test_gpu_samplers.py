@@ -127,3 +127,42 @@ def test_sample_moments_2e16():
     assert abs(en[cols, 1:].std() / P["mask_sd"] - 1) < 0.01
     assert abs(mn[:cols].std() / P["mlwe_sd"] - 1) < 0.02
     assert abs(mn[cols].std() / P["mask_mlwe_sd"] - 1) < 0.05
+
+
+def test_commit_sampled_two_stream_split():
+    """A sampled batch of >= 64 commits runs as two halves on two streams (the caller's and the
+    handle's auxiliary one, joined by events): equal, bit for bit, to the single-stream runs of
+    the same commits (rg_jindo_sample_dev + rg_jindo_commit_dev of the whole batch, and two
+    sub-batches of < 64 with their first_commit offsets), on a caller stream that is not the null
+    stream."""
+    import torch
+    name = "t10_b1"
+    P = PARAMS[name]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = jindo.NewProver(params, b"Jindo!")
+    B, nv, first = 70, 1000, 5
+    v = np.stack([make_v(q, nv, seed=400 + b) for b in range(B)])
+    seeds = _seeds(b"split")
+    sh = params.shapes(B)
+    z = lambda k: torch.zeros(sh[k], dtype=torch.int64, device="cuda")
+    keys = ("incom", "enc", "mlwe_out", "com")
+    st = torch.cuda.Stream()
+    a = {k: z(k) for k in keys}
+    dv = _t(v)
+    torch.cuda.synchronize()
+    prv.commit_sampled_dev(B, dv, nv, seeds, first, a["incom"], a["enc"], a["mlwe_out"], a["com"], st)
+    st.synchronize()
+    b_ = {k: z(k) for k in keys}
+    for lo, hi in ((0, 30), (30, B)):
+        prv.commit_sampled_dev(hi - lo, dv[lo:hi], nv, seeds, first + lo, b_["incom"][lo:hi], b_["enc"][lo:hi],
+                               b_["mlwe_out"][lo:hi], b_["com"][lo:hi])
+    r = {k: z(k) for k in ("last_row", "mask", "enc_noise", "mlwe_noise")}
+    prv.sample_dev(B, dv, nv, seeds, first, r["last_row"], r["mask"], r["enc_noise"], r["mlwe_noise"])
+    c = {k: z(k) for k in keys}
+    prv.commit_dev(B, dv, nv, r["last_row"], r["mask"], r["enc_noise"], r["mlwe_noise"], c["incom"], c["enc"],
+                   c["mlwe_out"], c["com"])
+    torch.cuda.synchronize()
+    for k in keys:
+        assert torch.equal(a[k], b_[k]), k
+        assert torch.equal(a[k], c[k]), k
