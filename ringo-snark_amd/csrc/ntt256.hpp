@@ -221,14 +221,22 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
   }
 }
 
-// One tile of 4 sub-transforms x 256 points.  LDS: 4 limb planes (u64) of [s][x] rows:
+// One tile of 4 sub-transforms x 256 points.  LDS: limb planes (u64) of [s][x] rows:
 //   COL: pitch 296, pad (x >> 3) for every exchange; ROW: pitch 288, pads 4(x>>5) (H<->M),
 //   (x>>3) (M<->L), (x>>5) (L<->H) -- conflict-free for ds_*_b64 half-wave groups (checked by
 //   enumeration, tools/nttlab/banks.py).
+// An exchange moves the 4 limb planes through an LDS image of RG_NTT256_PLANES planes: with 2,
+// two rounds of (put, barrier, get) of 2 planes each, so a 128-thread workgroup holds 18.9 KiB
+// instead of 37.9 KiB and occupancy is set by VGPRs (3-4 waves/SIMD), not LDS (2 waves/SIMD).
+#ifndef RG_NTT256_PLANES
+#define RG_NTT256_PLANES 2
+#endif
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP>
 __global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
   constexpr int PITCH = COL ? 296 : 288, PLANE = 4 * PITCH;
-  __shared__ uint64_t lds[4 * PLANE];
+  constexpr int NPL = RG_NTT256_PLANES;  // limb planes per LDS round (4 or 2)
+  static_assert(NPL == 4 || NPL == 2, "RG_NTT256_PLANES");
+  __shared__ uint64_t lds[NPL * PLANE];
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 3u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 2) : (tid & 31u);
@@ -268,18 +276,32 @@ __global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
     if (COL) return s * PITCH + x + (x >> 3);
     return s * PITCH + x + (ph == HM ? 4 * (x >> 5) : ph == ML ? (x >> 3) : (x >> 5));
   };
-  auto put = [&](int reg, uint32_t x, int ph) {
+  // limbs [l0, l0 + NPL) of register `reg` to / from LDS planes 0..NPL-1
+  auto put = [&](int reg, uint32_t x, int ph, int l0) {
     const uint32_t p = lpos(x, ph);
 #pragma unroll
-    for (int l = 0; l < 4; ++l) lds[l * PLANE + p] = pk(e[reg][2 * l], e[reg][2 * l + 1]);
+    for (int l = 0; l < NPL; ++l) lds[l * PLANE + p] = pk(e[reg][2 * (l0 + l)], e[reg][2 * (l0 + l) + 1]);
   };
-  auto get = [&](int reg, uint32_t x, int ph) {
+  auto get = [&](int reg, uint32_t x, int ph, int l0) {
     const uint32_t p = lpos(x, ph);
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
+    for (int l = 0; l < NPL; ++l) {
       const uint64_t v = lds[l * PLANE + p];
-      e[reg][2 * l] = lo32(v);
-      e[reg][2 * l + 1] = hi32(v);
+      e[reg][2 * (l0 + l)] = lo32(v);
+      e[reg][2 * (l0 + l) + 1] = hi32(v);
+    }
+  };
+  // registers written at positions px(i) (phase pp) are read back at positions gx(i) (phase gp);
+  // pre: the LDS image may still be read by an earlier exchange (barrier first)
+  auto xchg = [&](auto px, int pp, auto gx, int gp, bool pre) {
+#pragma unroll
+    for (int l0 = 0; l0 < 4; l0 += NPL) {
+      if (pre || l0 > 0) __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) put(i, px(i), pp, l0);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) get(i, gx(i), gp, l0);
     }
   };
   const bool rowuni = RP;
@@ -287,18 +309,9 @@ __global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) gload(y, xH(y));
     ntt256_round<3, 5, 0, false, false, COL>(a, twr, e, hi, t, rowuni);
-#pragma unroll
-    for (int y = 0; y < 8; ++y) put(y, xH(y), HM);
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; ++y) get(y, xM(y), HM);
+    xchg(xH, HM, xM, HM, false);
     ntt256_round<3, 2, 1, false, false, COL>(a, twr, e, hi, t, rowuni);
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; ++y) put(y, xM(y), ML);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) get(r, xL(r), ML);
+    xchg(xM, ML, xL, ML, true);
     ntt256_round<2, 0, 2, false, false, COL>(a, twr, e, hi, t, rowuni);
     if (CANON) {
 #pragma unroll
@@ -308,15 +321,9 @@ __global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) gstore(r, xL(r));
     } else {  // L -> H for coalesced rows
-      __syncthreads();
+      xchg(xL, LH, xH, LH, true);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) put(r, xL(r), LH);
-      __syncthreads();
-#pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        get(y, xH(y), LH);
-        gstore(y, xH(y));
-      }
+      for (int y = 0; y < 8; ++y) gstore(y, xH(y));
     }
   } else {
     if constexpr (COL) {
@@ -325,26 +332,12 @@ __global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
     } else {  // rows arrive coalesced in H, transpose to L
 #pragma unroll
       for (int y = 0; y < 8; ++y) gload(y, xH(y));
-#pragma unroll
-      for (int y = 0; y < 8; ++y) put(y, xH(y), LH);
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 8; ++r) get(r, xL(r), LH);
-      __syncthreads();
+      xchg(xH, LH, xL, LH, false);
     }
     ntt256_round<2, 0, 2, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) put(r, xL(r), ML);
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; ++y) get(y, xM(y), ML);
+    xchg(xL, ML, xM, ML, !COL);
     ntt256_round<3, 2, 1, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; ++y) put(y, xM(y), HM);
-    __syncthreads();
-#pragma unroll
-    for (int y = 0; y < 8; ++y) get(y, xH(y), HM);
+    xchg(xM, HM, xH, HM, true);
     ntt256_round<3, 5, 0, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
     if (CANON) {
 #pragma unroll
