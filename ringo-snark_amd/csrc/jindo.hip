@@ -1175,8 +1175,11 @@ __global__ __launch_bounds__(256 * JG, 1) void mac3h_kernel(Mac3Args a) {
 }
 
 // J padded to the instantiated widths
+#ifndef RG_MAC3_JP10
+#define RG_MAC3_JP10 0  // 0: J = 9..10 padded to JP = 12 (1,024-thread mac3h<12,4>) instead of mac3h<10,2>
+#endif
 static int mac3_jp(int J) {
-  static const int w[] = {4, 6, 8, 10, 12, 16};
+  static const int w[] = {4, 6, 8, RG_MAC3_JP10 ? 10 : 12, 12, 16};
   for (int x : w)
     if (J <= x) return x;
   return 0;

@@ -231,8 +231,11 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
 #ifndef RG_NTT256_PLANES
 #define RG_NTT256_PLANES 2
 #endif
+#ifndef RG_NTT256_WPE
+#define RG_NTT256_WPE 1  // amdgpu_waves_per_eu lower bound (A/B knob)
+#endif
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP>
-__global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_WPE))) void ntt256_pass(Ntt256Args a) {
   constexpr int PITCH = COL ? 296 : 288, PLANE = 4 * PITCH;
   constexpr int NPL = RG_NTT256_PLANES;  // limb planes per LDS round (4 or 2)
   static_assert(NPL == 4 || NPL == 2, "RG_NTT256_PLANES");
