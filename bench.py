@@ -119,6 +119,7 @@ PREWARM = [True]
 
 
 def prewarm(torch, fn, seconds=0.3):
+    seconds = float(os.environ.get("RINGO_PREWARM_S", seconds))
     """Untimed: run the step until the GPU has held its sustained clock for a while (the first
     ~20 steps of this integer-multiply-heavy load run 10-30% slower while power management
     settles; tools/nttlab/pass_lab 'ramp').  Returns the number of steps run."""
