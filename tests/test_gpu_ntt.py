@@ -174,3 +174,34 @@ def test_ntt_2e16_full_batch_spot_check(fields):
     T.inv_dev(x, x, B)
     torch.cuda.synchronize()
     assert torch.equal(x, ref)
+
+
+def test_ntt_2e16_q255_bench_batch_spot_check(fields):
+    """configs[3]'s full L = 4 batch as bench.py's l4 line runs it (64 polynomials of 2^16
+    Montgomery words at the Jindo default prime, 128 MiB, in place): polynomials 0, 37 and 63 of
+    the forward transform against the C oracle, then the inverse restores all 64 bit-exactly.
+    Covers the ntt256_pass same-row-of-4 ROW tiling at the batch the bench times."""
+    import torch
+    q = fields["jindo_zp"]
+    N, B = 1 << 16, 64
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, _, _ = cf.tables(N)
+    assert q > 1 << 254  # words below 2^254 are canonical residues (valid Montgomery forms)
+    rng = np.random.default_rng(255)
+    a = rng.integers(0, 2 ** 64, size=(B, N, F.L), dtype=np.uint64)
+    a[:, :, 3] >>= np.uint64(2)
+    a[63, N - 1] = F.mont([q - 1])[0]
+    x = torch.from_numpy(a.view(np.int64).reshape(-1).copy()).cuda()
+    ref = x.clone()
+    T.fwd_dev(x, x, B)
+    torch.cuda.synchronize()
+    picks = [0, 37, 63]
+    want = cf.ntt_fwd(np.ascontiguousarray(a[picks]), tw)
+    got = x.cpu().numpy().view(np.uint64).reshape(B, N, F.L)
+    for j, i in enumerate(picks):
+        assert (got[i] == want[j]).all(), i
+    T.inv_dev(x, x, B)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
