@@ -600,15 +600,20 @@ def main():
         PREWARM[0] = False
     import torch
 
+    ngpu = torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+    if world > ngpu or local >= ngpu:
+        print(f"bench.py: WORLD_SIZE={world} (LOCAL_RANK={local}) but {ngpu} visible GPU(s): one rank per GPU",
+              file=sys.stderr)
+        return 2
     dist = None
     if world > 1:
         import torch.distributed as tdist
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
-    torch.cuda.set_device(local)
     import ringo
+    from ringo.shard import bind_device
 
-    ringo.lib().rg_set_device(local)
+    bind_device(local, world)  # LOCAL_RANK -> torch and libringo's current device, checked
     C, csrc = counters()
     N = 1 << args.logn
     out = {}

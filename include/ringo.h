@@ -247,6 +247,12 @@ rg_status rg_jindo_commit_core_dev(const rg_jindo* j, size_t batch, const uint64
 /* Bytes of device scratch rg_jindo_commit_dev needs for `batch` commits (allocated on first
  * use and cached inside the handle, one set per stream; exposed for capacity planning). */
 size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
+/* Drop the scratch cached for `stream` (and for the library-owned stream that splits a sampled
+ * commit issued on it), after draining both.  Scratch sets are kept per stream for the handle's
+ * lifetime otherwise; a caller that creates streams per request calls this before destroying one
+ * (a destroyed stream's handle value may be reused by a new stream).  Not concurrent with calls
+ * on that stream. */
+rg_status rg_jindo_release_stream(rg_jindo* j, void* stream);
 
 /* ---- the prover's randomness on the device --------------------- */
 /* The standard deviations jindo.Parameters holds (params.go:99-111): ecdStdDev,
@@ -269,11 +275,16 @@ rg_status rg_jindo_delta_inv(const rg_jindo* j, double* out);
  * Prover.mlweSampler, Prover.roundedSampler, and `uniform` in place of crypto/rand for
  * MustSetRandom (prover.go:65-139, encoder.go:149-183).  A Go caller draws them from crypto/rand.
  * On the device each sampler instance is a window of its domain's counter space (instance n =
- * the UniformSampler with IV + n 2^24): one per encode polynomial (twinCDT), per MLWE
- * polynomial (mlweSampler), per sample (COSAC, rounded) and per field element (uniform),
- * numbered from `first_commit`, the index of the batch's first commit among all commits made
- * with these seeds (so batches and GPUs never share keystream).  Each instance is exactly the
- * reference's sampler; the partition of draws among instances is this library's. */
+ * the UniformSampler with IV + n 2^24, a 128-bit sum, so the 2^64 instance numbers have disjoint
+ * windows): one per encode polynomial (twinCDT), per MLWE polynomial (mlweSampler), per sample
+ * (COSAC, rounded) and per field element (uniform), numbered from `first_commit`, the index of
+ * the batch's first commit among all commits made with these seeds (so batches and GPUs never
+ * share keystream).  The sampled entry points return RG_ERR_INVALID when an instance number of
+ * commits [first_commit, first_commit + batch) would pass 2^64 - 1, i.e. when
+ * (first_commit + batch) * max((cols+1) rows d, (cols+1)(in_msis+mlwe) d, (cols+rows) slots) > 2^64.
+ * Each instance is exactly the reference's sampler; the partition of draws among instances is
+ * this library's.  Two provers (e.g. Go's SafeCopy, prover.go:327-339, which gives the copy new
+ * crypto/rand samplers) either hold their own seeds or disjoint first_commit ranges. */
 typedef struct {
   uint8_t enc_cdt[32], enc_cosac[32], enc_cosac_round[32], mlwe_cdt[32], mlwe_round[32], uniform[32];
 } rg_jindo_seeds;
@@ -369,6 +380,9 @@ rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream
 rg_status rg_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, void* stream);
 rg_status rg_stream_sync(void* stream);
 rg_status rg_set_device(int device);
+/* the calling thread's current device (one rank per GPU: LOCAL_RANK -> rg_set_device) */
+rg_status rg_get_device(int* device);
+rg_status rg_device_count(int* n);
 
 #ifdef __cplusplus
 }

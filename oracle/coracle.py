@@ -48,6 +48,9 @@ def lib():
                                       i64p, i64p]
         L.of_uniform_words.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_long,
                                        u64p]
+        L.of_sampler_draws.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_double, ctypes.c_double, ctypes.c_long,
+                                       ctypes.c_long, ctypes.POINTER(ctypes.c_int64)]
+        L.of_sampler_draws.restype = ctypes.c_int
         L.of_jindo_verify.restype = ctypes.c_int
         L.of_jindo_verify.argtypes = ([ctypes.c_void_p] + [u64p] * 3 + [ctypes.c_long] + [u64p] * 11 +
                                       [ctypes.c_double, ctypes.c_double, u64p, ctypes.POINTER(ctypes.c_int), u64p])
@@ -379,5 +382,16 @@ def uniform_words(seed, inst, first, n):
     """UniformSampler.Sample() words [first, first + n) of instance `inst` (oracle.c)."""
     out = np.zeros(n, np.uint64)
     if lib().of_uniform_words(bytes(seed), len(seed), inst, first, n, ptr(out)):
+        raise RuntimeError("libcrypto unavailable")
+    return out
+
+
+def sampler_draws(kind, seeds, sigma, center, n, per_inst=256):
+    """n draws of one reference sampler (oracle.c of_sampler_draws): kind "twin_cdt", "cosac" or
+    "rounded"; seeds = 64 bytes (the sampler's UniformSampler seed, then COSAC's rounded one)."""
+    k = {"twin_cdt": 0, "cosac": 1, "rounded": 2}[kind]
+    out = np.zeros(n, np.int64)
+    if lib().of_sampler_draws(k, bytes(seeds), float(sigma), float(center), n, per_inst,
+                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))):
         raise RuntimeError("libcrypto unavailable")
     return out

@@ -1623,6 +1623,32 @@ int of_jindo_sample(const of_jindo* J, const double* sd, const double* delta, co
   return 0;
 }
 
+/* n draws of one sampler (distribution tests): kind 0 TwinCDTGaussianSampler(sigma).Sample(center),
+ * 1 COSACSampler.Sample(center, sigma), 2 RoundedGaussianSampler.Sample(center, sigma).  Draw k
+ * reads instance k / per_inst of seeds[0..32) (and, for COSAC's rounded sampler, of
+ * seeds[32..64)), whose stream continues from draw to draw inside an instance. */
+int of_sampler_draws(int kind, const unsigned char* seeds, double sigma, double center, long n, long per_inst,
+                     int64_t* out) {
+  of_dom d0, d1;
+  if (dom_init(&d0, seeds, 32) || dom_init(&d1, seeds + 32, 32)) return -1;
+  if (!zkn[1] && !zkn[2]) zig_init();
+  of_cdt C;
+  C.tables = NULL;
+  if (kind == 0) cdt_init(&C, sigma);
+  of_uni B, R;
+  for (long k = 0; k < n; ++k) {
+    if (k % per_inst == 0) {
+      uni_init(&B, &d0, (uint64_t)(k / per_inst));
+      uni_init(&R, &d1, (uint64_t)(k / per_inst));
+    }
+    if (kind == 0) out[k] = cdt_sample(&C, &B, center);
+    else if (kind == 1) out[k] = cosac_sample(&B, &R, center, sigma);
+    else out[k] = (int64_t)round(center + norm_float(&B) * sigma);
+  }
+  free(C.tables);
+  return 0;
+}
+
 /* UniformSampler.Sample() words [first, first + n) of instance `inst` of the seed's sampler */
 int of_uniform_words(const unsigned char* seed, size_t seed_len, uint64_t inst, uint64_t first, long n, uint64_t* out) {
   of_dom D;

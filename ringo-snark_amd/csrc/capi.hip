@@ -88,4 +88,16 @@ rg_status rg_set_device(int device) {
   return RG_OK;
 }
 
+rg_status rg_get_device(int* device) {
+  if (!device) return RG_ERR_INVALID;
+  RG_HIP(hipGetDevice(device));
+  return RG_OK;
+}
+
+rg_status rg_device_count(int* n) {
+  if (!n) return RG_ERR_INVALID;
+  RG_HIP(hipGetDeviceCount(n));
+  return RG_OK;
+}
+
 }  // extern "C"

@@ -4,7 +4,7 @@
 // with a 128-bit big-endian counter; Sample() reads little-endian u64 words out of an 8192-byte
 // buffer that every refill XORs the next keystream chunk into (XORKeyStream(buf, buf)), so word
 // w of chunk c is KS_0[w] ^ ... ^ KS_c[w].  On the device a sampler INSTANCE is a window of one
-// domain's counter space: instance n starts at counter IV + n * 2^24 and is exactly the Go
+// domain's counter space: instance n (any u64) starts at counter IV + n * 2^24 (a 128-bit sum) and is exactly the Go
 // UniformSampler whose IV is that counter.  Words are computed on demand (one AES block per two
 // words); an instance rarely reads past its first 1024 words, and when it does the XOR of the
 // earlier chunks is recomputed.
@@ -87,16 +87,17 @@ __device__ __forceinline__ uint32_t te_b(const uint32_t* lds, uint32_t s, uint32
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + off);
 }
 
-// AES-256 of the counter block IV + n; returns the 16 keystream bytes as 4 big-endian words.
+// AES-256 of the counter block IV + n, n = nhi 2^64 + nlo (128-bit big-endian add, as Go's
+// crypto/cipher CTR increments the whole block); returns the 16 keystream bytes as 4 big-endian words.
 // Round column: Te0[a] ^ ror8 Te0[b] ^ ror16 Te0[c] ^ ror24 Te0[d] ^ k
 //             = Te0[a] ^ Te1[b] ^ ror16(Te0[c] ^ Te1[d] ^ rol16 k)   (rotation is linear in ^)
 // = 4 v_perm + 2 v_bitop3 + 1 rotate per column.
 template <class K>
-__device__ __forceinline__ void aes_ctr(const K& key, uint64_t n, const uint32_t* lds, uint32_t out[4]) {
+__device__ __forceinline__ void aes_ctr(const K& key, uint64_t nhi, uint64_t nlo, const uint32_t* lds, uint32_t out[4]) {
   const uint32_t l0 = (threadIdx.x & 31u) << 2, l1 = l0 | 0x80u;
   const uint64_t ivlo = ((uint64_t)key.iv(2) << 32) | key.iv(3), ivhi = ((uint64_t)key.iv(0) << 32) | key.iv(1);
-  const uint64_t lo = ivlo + n;
-  const uint64_t hi = ivhi + (lo < n ? 1u : 0u);
+  const uint64_t lo = ivlo + nlo;
+  const uint64_t hi = ivhi + nhi + (lo < nlo ? 1u : 0u);
   uint32_t s0 = (uint32_t)(hi >> 32) ^ key.rk(0), s1 = (uint32_t)hi ^ key.rk(1), s2 = (uint32_t)(lo >> 32) ^ key.rk(2),
            s3 = (uint32_t)lo ^ key.rk(3);
   auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kr) {
@@ -125,26 +126,31 @@ __device__ __forceinline__ void aes_ctr(const K& key, uint64_t n, const uint32_t
   out[3] = fin(s3, s0, s1, s2, key.rk(59));
 }
 
-// the two little-endian u64 keystream words of block n
+// The two little-endian u64 keystream words of block `off` of instance `inst`'s window, i.e. of
+// counter block IV + inst 2^24 + off.  inst 2^24 is formed in 128 bits (hi = inst >> 40): an
+// instance number up to 2^64 - 1 never wraps onto another instance's window (oracle.c uni_init).
 template <class K>
-__device__ __forceinline__ void ks_words(const K& key, uint64_t n, const uint32_t* lds, uint64_t& w0, uint64_t& w1) {
+__device__ __forceinline__ void ks_words(const K& key, uint64_t inst, uint64_t off, const uint32_t* lds, uint64_t& w0,
+                                         uint64_t& w1) {
+  const uint64_t wlo = inst << kWinShift, lo = wlo + off;
+  const uint64_t hi = (inst >> (64 - kWinShift)) + (lo < wlo ? 1u : 0u);
   uint32_t o[4];
-  aes_ctr(key, n, lds, o);
+  aes_ctr(key, hi, lo, lds, o);
   w0 = (uint64_t)bswap32(o[0]) | ((uint64_t)bswap32(o[1]) << 32);
   w1 = (uint64_t)bswap32(o[2]) | ((uint64_t)bswap32(o[3]) << 32);
 }
-__device__ __forceinline__ void ks_words(const AesKey& K, uint64_t n, const uint32_t* lds, uint64_t& w0, uint64_t& w1) {
-  ks_words(ArgKey{K}, n, lds, w0, w1);
+__device__ __forceinline__ void ks_words(const AesKey& K, uint64_t inst, uint64_t off, const uint32_t* lds, uint64_t& w0,
+                                         uint64_t& w1) {
+  ks_words(ArgKey{K}, inst, off, lds, w0, w1);
 }
 
-// word `p` of the Sample() stream of the instance whose window starts at block `base`
-// (uniform.go:64-82): chunk c = KS_0 ^ ... ^ KS_c
-__device__ __noinline__ uint64_t uniform_word_at(LdsKey key, const uint32_t* lds, uint64_t base, uint64_t p) {
+// word `p` of the Sample() stream of instance `inst` (uniform.go:64-82): chunk c = KS_0 ^ ... ^ KS_c
+__device__ __noinline__ uint64_t uniform_word_at(LdsKey key, const uint32_t* lds, uint64_t inst, uint64_t p) {
   const uint64_t c = p >> 10, o = p & 1023u;
   uint64_t x = 0;
   for (uint64_t i = 0; i <= c; ++i) {
     uint64_t w0, w1;
-    ks_words(key, base + ((i << 10) + o) / 2, lds, w0, w1);
+    ks_words(key, inst, ((i << 10) + o) / 2, lds, w0, w1);
     x ^= (o & 1) ? w1 : w0;
   }
   return x;
@@ -154,19 +160,19 @@ __device__ __noinline__ uint64_t uniform_word_at(LdsKey key, const uint32_t* lds
 struct Uniform {
   LdsKey key;
   const uint32_t* lds;
-  uint64_t base;  // first block of the window
+  uint64_t inst;  // the instance (its window starts at block inst 2^24)
   uint64_t pos;   // next word
   uint64_t spare;
   bool have_spare;
 
-  __device__ __forceinline__ void init(const uint32_t* key_lds, const uint32_t* l, uint64_t inst) {
+  __device__ __forceinline__ void init(const uint32_t* key_lds, const uint32_t* l, uint64_t instance) {
     key.p = key_lds;
     lds = l;
-    base = inst << kWinShift;
+    inst = instance;
     pos = 0;
     have_spare = false;
   }
-  __device__ uint64_t word_at(uint64_t p) const { return uniform_word_at(key, lds, base, p); }
+  __device__ uint64_t word_at(uint64_t p) const { return uniform_word_at(key, lds, inst, p); }
   __device__ __forceinline__ uint64_t sample() {
     uint64_t r;
     if (have_spare) {
@@ -174,7 +180,7 @@ struct Uniform {
       have_spare = false;
     } else if (pos < 1024 && !(pos & 1)) {
       uint64_t w0, w1;
-      ks_words(key, base + pos / 2, lds, w0, w1);
+      ks_words(key, inst, pos / 2, lds, w0, w1);
       r = w0;
       spare = w1;
       have_spare = true;

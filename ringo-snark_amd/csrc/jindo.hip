@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
   const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
   if (sd == a.sd_ecd) {  // Encoder.twinCDT (encoder.go:169-170): one word per sample
     uint64_t w0, w1;
-    ks_words(a.key[kDomEncCdt], (gpoly << kWinShift) + (uint64_t)m, lds, w0, w1);
+    ks_words(a.key[kDomEncCdt], gpoly, (uint64_t)m, lds, w0, w1);
     out[2 * m] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m), w0);
     out[2 * m + 1] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m + 1), w1);
   } else {  // Encoder.cosac (encoder.go:171-172)
@@ -1725,8 +1725,8 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
 #if RG_VAR & 2
     for (int h = 0; h < 4; ++h) u[h] = (gpoly * 0x9E3779B97F4A7C15ull + (uint64_t)(4 * lane + h)) * 0xBF58476D1CE4E5B9ull;
 #else
-    ks_words(key, (gpoly << kWinShift) + (uint64_t)(2 * lane), lds, u[0], u[1]);
-    ks_words(key, (gpoly << kWinShift) + (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
+    ks_words(key, gpoly, (uint64_t)(2 * lane), lds, u[0], u[1]);
+    ks_words(key, gpoly, (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
 #endif
     // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111)
     int tab[8], v[8];
@@ -2013,11 +2013,10 @@ __device__ __forceinline__ bool cosac_fast(const LdsKey& kb, const LdsKey& kr, c
                                            unsigned long long inst, double center, double sd, const ZigDev& Z,
                                            long long& res) {
   uint64_t bw[2 * KB], rw[2 * KR];
-  const uint64_t w0 = inst << kWinShift;
 #pragma unroll
-  for (int i = 0; i < KB; ++i) ks_words(kb, w0 + i, lds, bw[2 * i], bw[2 * i + 1]);
+  for (int i = 0; i < KB; ++i) ks_words(kb, inst, (uint64_t)i, lds, bw[2 * i], bw[2 * i + 1]);
 #pragma unroll
-  for (int i = 0; i < KR; ++i) ks_words(kr, w0 + i, lds, rw[2 * i], rw[2 * i + 1]);
+  for (int i = 0; i < KR; ++i) ks_words(kr, inst, (uint64_t)i, lds, rw[2 * i], rw[2 * i + 1]);
   const double two_s2 = 2.0 * sd * sd;
   const double lead = sqrt(2.0 * M_PI) * sd;
   const double c_int = round(center);
@@ -2216,11 +2215,11 @@ __global__ __launch_bounds__(kCosacThreads) void cosac_noise_kernel(SampleArgs a
       const uint64_t p = L.pos[s];
       uint64_t w0, w1;
       if (p < 1024) {
-        ks_words(LdsKey{keys[s]}, (L.inst << kWinShift) + p / 2, lds, w0, w1);
+        ks_words(LdsKey{keys[s]}, L.inst, p / 2, lds, w0, w1);
         L.spare[s] = w1;
         L.have[s] = true;
       } else {  // past the first 8 KiB buffer: the XOR-accumulated refill (rare)
-        w0 = uniform_word_at(LdsKey{keys[s]}, lds, L.inst << kWinShift, p);
+        w0 = uniform_word_at(LdsKey{keys[s]}, lds, L.inst, p);
       }
       ++L.pos[s];
       cosac_step(L, w0, Z);
@@ -2248,7 +2247,7 @@ __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * nm + (unsigned long long)poly;
   if (col != S.cols) {  // mlweSampler.Sample(0): centre 0, one table, no float tail
     uint64_t w0, w1;
-    ks_words(a.key[kDomMlweCdt], (gpoly << kWinShift) + (uint64_t)m, lds, w0, w1);
+    ks_words(a.key[kDomMlweCdt], gpoly, (uint64_t)m, lds, w0, w1);
     out[2 * m] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0) + a.cdt_mlwe.tail_lo;
     out[2 * m + 1] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1) + a.cdt_mlwe.tail_lo;
   } else {  // roundedSampler.Sample(0, maskMLWEStdDev)
@@ -2301,15 +2300,15 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
   }
   const unsigned long long inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
   if ((L % 2) == 0 && a.kbytes == 8 * L) {  // whole words (e.g. q255: 32 bytes): a try = L/2 blocks, in parallel
-    const uint64_t base = (uint64_t)inst << kWinShift, topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
+    const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
     for (uint64_t t = 0;; ++t) {
       uint64_t z[L];
       if ((t + 1) * L <= 1024) {
 #pragma unroll
-        for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, base + t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
+        for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, inst, t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
       } else {  // past the first 8 KiB buffer (uniform.go:64-82)
 #pragma unroll
-        for (int l = 0; l < L; ++l) z[l] = uniform_word_at(LdsKey{key}, lds, base, t * L + l);
+        for (int l = 0; l < L; ++l) z[l] = uniform_word_at(LdsKey{key}, lds, inst, t * L + l);
       }
       z[L - 1] &= topm;  // the last byte's unused top bits (element.go:320-325)
       if (!geq_q<L>(z, a.F)) {
@@ -2597,9 +2596,11 @@ struct rg_jindo {
   std::mutex mu;  // guards `scratch` and `aux`
   std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
   rg_jindo_samplers smp;
-  hipStream_t aux = nullptr;  // second stream of the sampled commit's two-way split (lazily created)
+  // second stream of the sampled commit's two-way split, one per caller stream (lazily created), so
+  // that its scratch (keyed by the aux stream) belongs to that caller stream alone
+  std::map<hipStream_t, hipStream_t> aux;
   ~rg_jindo() {
-    if (aux) (void)hipStreamDestroy(aux);
+    for (auto& kv : aux) (void)hipStreamDestroy(kv.second);
   }
 };
 
@@ -3876,11 +3877,30 @@ rg_status rg_jindo_delta_inv(const rg_jindo* J, double* out) {
   return RG_OK;
 }
 
+// Every sampler instance of commits [first, first + batch) must have a u64 number (so that no two
+// instances share a window; csprng.hpp ks_words): the largest per-commit count of a domain is
+// (cols+1) rows d (COSAC, per sample), (cols+1) (in_msis+mlwe) d (rounded MLWE, per sample) or
+// (cols + rows) slots (MustSetRandom, per element).
+static rg_status instances_in_range(const rg_jindo* J, unsigned long long first, size_t batch) {
+  const rg_jindo_params& p = J->p;
+  const unsigned __int128 per_enc = (unsigned __int128)(p.cols + 1) * p.rows * p.d;
+  const unsigned __int128 per_ml = (unsigned __int128)(p.cols + 1) * (p.in_msis + p.mlwe) * p.d;
+  const unsigned __int128 per_uni = (unsigned __int128)(p.cols + p.rows) * p.slots;
+  const unsigned __int128 per = std::max(per_enc, std::max(per_ml, per_uni));
+  const unsigned __int128 end = (unsigned __int128)first + batch;
+  if (end > ((unsigned __int128)1 << 64) / per) {
+    set_last_error("first_commit + batch: sampler instance numbers would exceed 2^64");
+    return RG_ERR_INVALID;
+  }
+  return RG_OK;
+}
+
 rg_status rg_jindo_sample_dev(const rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv,
                               const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_last_row,
                               uint64_t* d_mask, int64_t* d_enc_noise, int64_t* d_mlwe_noise, void* stream) {
   if (!J || !seeds) return RG_ERR_INVALID;
   if (nv < 1 || nv > (size_t)J->p.rank) return RG_ERR_RANK;
+  RG_TRY(instances_in_range(J, first_commit, batch));
   if (batch == 0) return RG_OK;
   if (!d_v || !d_last_row || !d_mask || !d_enc_noise || !d_mlwe_noise) return RG_ERR_INVALID;
   RG_TRY(on_device(J));
@@ -3897,6 +3917,7 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
                                       uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream) {
   if (!J || !seeds) return RG_ERR_INVALID;
   if (nv < 1 || nv > (size_t)J->p.rank) return RG_ERR_RANK;
+  RG_TRY(instances_in_range(J, first_commit, batch));
   if (batch == 0) return RG_OK;
   if (!d_v || !d_incom || !d_enc || !d_mlwe || !d_com) return RG_ERR_INVALID;
   RG_TRY(on_device(J));
@@ -3918,13 +3939,16 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   // Two halves on two streams (the caller's and the handle's auxiliary one, joined by events):
   // the samplers (LDS / AES-latency bound) of one half overlap the other half's VALU-bound core
   // (tools/stream_overlap.py: +4-5% commits/s).  Results are identical: sampler instances are
-  // numbered per commit (first_commit + b0), scratch is per stream.
+  // numbered per commit (first_commit + b0), scratch is per stream, and the aux stream (with its
+  // scratch) belongs to this caller stream only, so concurrent callers on different streams never
+  // share a buffer.
   if (batch < 64) return run(0, batch, st);
   hipStream_t aux;
   {
     std::lock_guard<std::mutex> lk(Jm->mu);
-    if (!Jm->aux) RG_HIP(hipStreamCreateWithFlags(&Jm->aux, hipStreamNonBlocking));
-    aux = Jm->aux;
+    hipStream_t& a = Jm->aux[st];
+    if (!a) RG_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+    aux = a;
   }
   hipEvent_t e0, e1;
   RG_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
@@ -3939,6 +3963,23 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return s1;
+}
+
+rg_status rg_jindo_release_stream(rg_jindo* J, void* stream) {
+  if (!J) return RG_ERR_INVALID;
+  RG_TRY(on_device(J));
+  hipStream_t st = as_stream(stream);
+  std::lock_guard<std::mutex> lk(J->mu);
+  RG_HIP(hipStreamSynchronize(st));
+  auto a = J->aux.find(st);
+  if (a != J->aux.end()) {
+    RG_HIP(hipStreamSynchronize(a->second));
+    J->scratch.erase(a->second);
+    (void)hipStreamDestroy(a->second);
+    J->aux.erase(a);
+  }
+  J->scratch.erase(st);
+  return RG_OK;
 }
 
 rg_status rg_uniform_words_dev(const uint8_t* seed, size_t seed_len, unsigned long long instance,

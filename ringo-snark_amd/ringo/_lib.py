@@ -105,6 +105,7 @@ _SIGS = {
     "rg_jindo_commit_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp,
                                            vp]),
     "rg_jindo_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
+    "rg_jindo_release_stream": (ctypes.c_int, [vp, vp]),
     "rg_jindo_eval_batch_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "rg_jindo_eval_partial_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "rg_jindo_eval_reduce_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
@@ -118,6 +119,8 @@ _SIGS = {
     "rg_memcpy_d2d": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp]),
     "rg_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "rg_get_device": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "rg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
 }
 
 

@@ -245,6 +245,10 @@ class Prover:
                                                 _addr(enc, _words(sh["enc"])), _addr(mlwe, _words(sh["mlwe_out"])),
                                                 _addr(com, _words(sh["com"])), _stream(stream)))
 
+    def release_stream(self, stream=None):
+        """Drop the scratch the handle caches for `stream` (rg_jindo_release_stream)."""
+        check(lib().rg_jindo_release_stream(self.h, _stream(stream)))
+
     def commit_core(self, enc, mlwe):
         """The Ajtai core of Commit (prover.go:144-202) from NTT-domain Opening.Encode / MLWE:
         returns (Commitment.Value, Opening.InCommit)."""
@@ -277,22 +281,35 @@ class Prover:
     def eval_batch_dev(self, batch, incom, enc, mlwe, bq, bo, ob_incom, ob_enc, ob_mlwe, stream=None):
         """openBatch = sum_i open[i] * batch[i] (prover.go:228-269); Proof.InCommit = ob_incom.
         bq = bo = None (params.batch == 1): openBatch = open[0]."""
-        check(lib().rg_jindo_eval_batch_dev(self.h, batch, _addr(incom), _addr(enc), _addr(mlwe), _addr(bq),
-                                            _addr(bo), _addr(ob_incom), _addr(ob_enc), _addr(ob_mlwe),
+        P, sh, es = self.params, self.params.shapes(batch), self.eval_shapes()
+        w = lambda k: _words(sh[k])
+        check(lib().rg_jindo_eval_batch_dev(self.h, batch, _addr(incom, w("incom")), _addr(enc, w("enc")),
+                                            _addr(mlwe, w("mlwe_out")), _addr(bq, batch * P.nq * P.d),
+                                            _addr(bo, batch * P.nqo * P.d), _addr(ob_incom, _words(es["ob_incom"])),
+                                            _addr(ob_enc, _words(es["ob_enc"])), _addr(ob_mlwe, _words(es["ob_mlwe"])),
                                             _stream(stream)))
 
     def eval_reduce_dev(self, ob_incom, ob_enc, ob_mlwe, stream=None):
         """Words mod q in place (after summing partial openBatches across GPUs)."""
-        check(lib().rg_jindo_eval_reduce_dev(self.h, _addr(ob_incom), _addr(ob_enc), _addr(ob_mlwe), _stream(stream)))
+        es = self.eval_shapes()
+        check(lib().rg_jindo_eval_reduce_dev(self.h, _addr(ob_incom, _words(es["ob_incom"])),
+                                             _addr(ob_enc, _words(es["ob_enc"])), _addr(ob_mlwe, _words(es["ob_mlwe"])),
+                                             _stream(stream)))
 
     def eval_partial_dev(self, ob_enc, left, partial, stream=None):
         """Proof.Partial[0..cols) and PartialMask (= partial[cols]) (prover.go:274-282)."""
-        check(lib().rg_jindo_eval_partial_dev(self.h, _addr(ob_enc), _addr(left), _addr(partial), _stream(stream)))
+        P, es = self.params, self.eval_shapes()
+        check(lib().rg_jindo_eval_partial_dev(self.h, _addr(ob_enc, _words(es["ob_enc"])),
+                                              _addr(left, P.rows * P.nq * P.d), _addr(partial, _words(es["partial"])),
+                                              _stream(stream)))
 
     def eval_respond_dev(self, ob_enc, ob_mlwe, chals, pf_enc, pf_mlwe, stream=None):
         """Proof.Encode and Proof.MLWE (prover.go:300-314)."""
-        check(lib().rg_jindo_eval_respond_dev(self.h, _addr(ob_enc), _addr(ob_mlwe), _addr(chals), _addr(pf_enc),
-                                              _addr(pf_mlwe), _stream(stream)))
+        P, es = self.params, self.eval_shapes()
+        check(lib().rg_jindo_eval_respond_dev(self.h, _addr(ob_enc, _words(es["ob_enc"])),
+                                              _addr(ob_mlwe, _words(es["ob_mlwe"])), _addr(chals, P.cols * P.nq * P.d),
+                                              _addr(pf_enc, _words(es["pf_enc"])), _addr(pf_mlwe, _words(es["pf_mlwe"])),
+                                              _stream(stream)))
 
 
 class VerifyResultC(ctypes.Structure):  # include/ringo.h rg_jindo_verify_result
@@ -332,9 +349,13 @@ class Verifier:
         if P.res_two_nm is None or P.in_com_dcmp_two_nm is None:
             raise RingoPanic("Parameters lack the two-norm bounds")
         r = VerifyResultC()
-        check(lib().rg_jindo_verify_dev(self.h, batch, _addr(com), _addr(bq), _addr(bo), _addr(chals), _addr(left),
-                                        _addr(right), _addr(y), _addr(pf_incom), _addr(pf_partial), _addr(pf_enc),
-                                        _addr(pf_mlwe), float(P.in_com_dcmp_two_nm), float(P.res_two_nm),
+        nm, pq = P.in_msis + P.mlwe, P.nq * P.d
+        check(lib().rg_jindo_verify_dev(self.h, batch, _addr(com, batch * P.out_msis * pq), _addr(bq, batch * pq),
+                                        _addr(bo, batch * P.nqo * P.d), _addr(chals, P.cols * pq),
+                                        _addr(left, P.rows * pq), _addr(right, P.cols * P.slots * P.L),
+                                        _addr(y, batch * P.L), _addr(pf_incom, P.dcmp * P.nqo * P.d),
+                                        _addr(pf_partial, (P.cols + 1) * pq), _addr(pf_enc, P.rows * pq),
+                                        _addr(pf_mlwe, nm * pq), float(P.in_com_dcmp_two_nm), float(P.res_two_nm),
                                         ctypes.byref(r), _stream(stream)))
         word = lambda w: sum(int(x) << (64 * i) for i, x in enumerate(w))
         L = P.L

@@ -2,6 +2,8 @@
 is RCCL on ROCm), independent polynomials / commitments sharded in contiguous ranges with no
 data-path collective, and ONE collective at setup: the commit key is broadcast
 from rank 0 over xGMI (or regenerated from the CRS per rank, which needs no collective)."""
+import ctypes
+
 import numpy as np
 
 
@@ -10,6 +12,24 @@ def shard_range(n_units, rank, world):
     base, extra = divmod(n_units, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+def bind_device(local_rank, world_size=1):
+    """One rank per GPU: LOCAL_RANK -> torch's current device and libringo's (rg_set_device), then
+    check both agree.  Fails (ValueError) when the node has fewer visible GPUs than ranks need."""
+    import torch
+    from ._lib import check, lib
+    n = torch.cuda.device_count()
+    if n < 1 or local_rank >= n:
+        raise ValueError(f"LOCAL_RANK {local_rank} (world {world_size}) but {n} visible GPU(s)")
+    torch.cuda.set_device(local_rank)
+    check(lib().rg_set_device(local_rank))
+    got = ctypes.c_int(-1)
+    check(lib().rg_get_device(ctypes.byref(got)))
+    if got.value != local_rank or torch.cuda.current_device() != local_rank:
+        raise RuntimeError(f"rank bound to device {got.value} / torch {torch.cuda.current_device()}, "
+                           f"want {local_rank}")
+    return local_rank
 
 
 def broadcast_commit_key(ck, dist, device=None, src=0):
@@ -69,7 +89,7 @@ def allreduce_open_batch(prv, dist, ob_incom, ob_enc, ob_mlwe, stream=None):
     buffer (exact: world * q < 2^64 for the <= 60-bit ring primes) and folded mod q on device.
     The tensors are int64 views of the uint64 words; they hold the full openBatch afterwards."""
     import torch
-    if dist is None or dist.get_world_size() == 1:
+    if dist is None:
         return
     P = prv.params
     assert dist.get_world_size() * max(max(P.q), max(P.qo)) < 2 ** 64

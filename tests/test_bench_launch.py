@@ -37,3 +37,16 @@ def test_launcher_runs_n_ranks(n):
 def test_world_size_mismatch_fails():
     p = _run(["--gpus", "2", "--plumbing"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.timeout(240)
+def test_more_ranks_than_gpus_fails():
+    """A real (non-plumbing) run whose WORLD_SIZE exceeds the visible GPUs stops before any
+    collective, with a message naming both (here: 0 GPUs in this container; on a GPU box the same
+    check refuses N > device_count)."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("needs a host with fewer than 2 visible GPUs")
+    p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-extra", "--no-cpu"])
+    assert p.returncode != 0
+    assert "visible GPU(s)" in p.stderr, p.stderr[-2000:]

@@ -63,7 +63,8 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(0)
+    from ringo.shard import bind_device
+    assert bind_device(0, world) == 0  # one card: every rank's LOCAL_RANK -> device 0
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ringo import jindo
     from ringo.shard import allreduce_open_batch, broadcast_prover, shard_range
@@ -106,3 +107,57 @@ def test_two_ranks_broadcast_commit_evaluate():
         assert d["com"] == com[d["lo"]:d["hi"]].tobytes(), r  # the shard's commitments
         assert d["ob"] == whole, r  # the all-reduced openBatch
     assert out[0]["hi"] == out[1]["lo"]
+
+
+def _rccl_worker(rank, world, port, out):
+    """world 1 on the `nccl` backend (RCCL): the exact calls bench.py makes on an N-GPU node
+    (init_process_group("nccl", device_id=...), bind_device, broadcast_prover's device-buffer
+    broadcast, allreduce_open_batch's all-reduce of device words + the mod-q fold), on real RCCL
+    collectives over device pointers.  One card cannot host two RCCL ranks (RCCL refuses a
+    duplicate GPU), so the multi-rank data movement is the gloo test above."""
+    import sys
+    root = os.path.dirname(HERE)
+    for p in (os.path.join(root, "ringo-snark_amd"), os.path.join(root, "oracle"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from ringo.shard import bind_device
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    bind_device(0, world)
+    from ringo import jindo
+    from ringo.shard import allreduce_open_batch, broadcast_prover
+    P = json.load(open(os.path.join(HERE, "golden", "jindo_params.json")))["t10_b8"]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = broadcast_prover(params, dist, b"Jindo!")
+    nv, vs, rnd, bq, bo = _inputs(P, q)
+    o, ob = _run(prv, params, 0, P["batch"], nv, vs, rnd, bq, bo)
+    before = b"".join(ob[k].cpu().numpy().tobytes() for k in ("ob_incom", "ob_enc", "ob_mlwe"))
+    allreduce_open_batch(prv, dist, ob["ob_incom"], ob["ob_enc"], ob["ob_mlwe"])
+    torch.cuda.synchronize()
+    out[rank] = {"com": o["com"].cpu().numpy().tobytes(), "before": before,
+                 "ob": b"".join(ob[k].cpu().numpy().tobytes() for k in ("ob_incom", "ob_enc", "ob_mlwe")),
+                 "ck": b"".join(np.ascontiguousarray(x).tobytes() for x in prv.commit_key())}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_rccl_single_rank_bench_path():
+    from ringo import jindo
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_worker, args=(1, _free_port(), out), nprocs=1, join=True)
+    P = json.load(open(os.path.join(HERE, "golden", "jindo_params.json")))["t10_b8"]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = jindo.NewProver(params, b"Jindo!")
+    nv, vs, rnd, bq, bo = _inputs(P, q)
+    o, ob = _run(prv, params, 0, P["batch"], nv, vs, rnd, bq, bo)
+    d = out[0]
+    assert d["ck"] == b"".join(np.ascontiguousarray(x).tobytes() for x in prv.commit_key())
+    assert d["com"] == o["com"].cpu().numpy().tobytes()
+    whole = b"".join(ob[k].cpu().numpy().tobytes() for k in ("ob_incom", "ob_enc", "ob_mlwe"))
+    assert d["before"] == whole and d["ob"] == whole  # all-reduce over one rank + fold: identity

@@ -30,7 +30,8 @@ def _h(t):
     return t.cpu().numpy()
 
 
-@pytest.mark.parametrize("inst,first,n", [(0, 0, 3000), (5, 1000, 100), (1 << 30, 2040, 20)])
+@pytest.mark.parametrize("inst,first,n", [(0, 0, 3000), (5, 1000, 100), (1 << 30, 2040, 20), ((1 << 40) + 3, 0, 1100),
+                                           (1 << 41, 1020, 40), ((1 << 64) - 1, 0, 70)])
 def test_uniform_words_match_oracle(inst, first, n):
     import torch
     seed = b"Jindo!"
@@ -54,7 +55,12 @@ def _seeds(tag):
 
 @pytest.mark.parametrize("name,B,nv,first", [("t10_b1", 2, None, 3), ("t10_b1", 1, 300, 0), ("t10_b8", 3, 700, 11),
                                              ("mult_t8193_b12", 1, None, 0), ("t14_b1", 1, None, 5),
-                                             ("t16_b4096", 1, 40000, 511)])
+                                             ("t16_b4096", 1, 40000, 511),
+                                             # COSAC instances past 2^40 (the window start carries into
+                                             # the counter's high word) ...
+                                             ("t16_b4096", 1, 40000, 940000),
+                                             # ... and the last commit whose instances fit in a u64
+                                             ("t16_b4096", 1, 40000, (1 << 64) // (9 * 513 * 256) - 1)])
 def test_sample_matches_oracle(name, B, nv, first):
     import torch
     P = PARAMS[name]
@@ -166,3 +172,85 @@ def test_commit_sampled_two_stream_split():
     for k in keys:
         assert torch.equal(a[k], b_[k]), k
         assert torch.equal(a[k], c[k]), k
+
+
+def test_first_commit_range_rejected():
+    """The sampled entry points refuse a first_commit whose instance numbers would pass 2^64 - 1
+    (include/ringo.h rg_jindo_seeds); the last one that fits is accepted."""
+    import torch
+    from ringo._lib import RingoError
+    P = PARAMS["t10_b1"]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = jindo.NewProver(params, b"Jindo!")
+    per = (P["cols"] + 1) * P["rows"] * P["d"]  # the largest per-commit instance count here
+    assert per >= (P["cols"] + 1) * (P["in_msis"] + P["mlwe"]) * P["d"]
+    v = make_v(q, 64, seed=5)[None]
+    sh = params.shapes(1)
+    o = {k: torch.zeros(sh[k], dtype=torch.int64, device="cuda") for k in ("last_row", "mask", "enc_noise", "mlwe_noise")}
+    last_ok = (1 << 64) // per - 1
+    prv.sample_dev(1, _t(v), 64, _seeds(b"range"), last_ok, o["last_row"], o["mask"], o["enc_noise"], o["mlwe_noise"])
+    torch.cuda.synchronize()
+    for first in (last_ok + 1, (1 << 64) - 1):
+        with pytest.raises(RingoError):
+            prv.sample_dev(1, _t(v), 64, _seeds(b"range"), first, o["last_row"], o["mask"], o["enc_noise"],
+                           o["mlwe_noise"])
+    sc = params.shapes(1)
+    z = {k: torch.zeros(sc[k], dtype=torch.int64, device="cuda") for k in ("incom", "enc", "mlwe_out", "com")}
+    with pytest.raises(RingoError):
+        prv.commit_sampled_dev(1, _t(v), 64, _seeds(b"range"), last_ok + 1, z["incom"], z["enc"], z["mlwe_out"],
+                               z["com"])
+
+
+def test_commit_sampled_concurrent_streams():
+    """Two host threads issue sampled batches of different sizes (64 and 160: both split over an
+    auxiliary stream) on their own streams at once; each result equals the same batch run alone on
+    the default stream, bit for bit (the auxiliary stream and its scratch belong to the caller
+    stream).  Then each stream's scratch is released and the handle still works."""
+    import threading
+    import torch
+    P = PARAMS["t10_b1"]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = jindo.NewProver(params, b"Jindo!")
+    nv = 500
+    keys = ("incom", "enc", "mlwe_out", "com")
+    jobs = []
+    for i, B in enumerate((64, 160)):
+        v = _t(np.stack([make_v(q, nv, seed=700 + 17 * i + b) for b in range(B)]))
+        sh = params.shapes(B)
+        jobs.append(dict(B=B, v=v, first=1000 * i, st=torch.cuda.Stream(), sh=sh,
+                         out={k: torch.zeros(sh[k], dtype=torch.int64, device="cuda") for k in keys}))
+    torch.cuda.synchronize()
+    errs = []
+    dev = torch.cuda.current_device()
+
+    def work(j):
+        try:
+            torch.cuda.set_device(dev)
+            for _ in range(3):  # repeated, so the two callers' launches interleave
+                prv.commit_sampled_dev(j["B"], j["v"], nv, _seeds(b"conc"), j["first"], *[j["out"][k] for k in keys],
+                                       stream=j["st"])
+            j["st"].synchronize()
+        except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(j,)) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for j in jobs:
+        ref = {k: torch.zeros(j["sh"][k], dtype=torch.int64, device="cuda") for k in keys}
+        prv.commit_sampled_dev(j["B"], j["v"], nv, _seeds(b"conc"), j["first"], *[ref[k] for k in keys])
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(j["out"][k], ref[k]), (j["B"], k)
+    for j in jobs:
+        prv.release_stream(j["st"])
+    again = {k: torch.zeros(jobs[0]["sh"][k], dtype=torch.int64, device="cuda") for k in keys}
+    prv.commit_sampled_dev(64, jobs[0]["v"], nv, _seeds(b"conc"), 0, *[again[k] for k in keys], stream=jobs[0]["st"])
+    jobs[0]["st"].synchronize()
+    for k in keys:
+        assert torch.equal(again[k], jobs[0]["out"][k]), k
