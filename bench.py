@@ -49,6 +49,10 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs; sustained shader clock under
 VALU_CYCLES = 4.5  # mean issue cost (cycles / wave64 instruction / SIMD) of the half-rate 64-bit
                    # integer ops these kernels are made of (tools/ubench)
 STEPS_DONE = {}  # line -> steps executed incl. prewarm/warmup (for per-step PMC attribution)
+try:  # per-kernel mean VALU issue cost of this library's static instruction mix (tools/valu_mix.py)
+    VALU_MIX = json.load(open(os.path.join(ROOT, "profiles", "valu_mix.json")))
+except (OSError, ValueError):
+    VALU_MIX = {}
 
 
 def splitmix64(seed, n):
@@ -167,7 +171,28 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     wall = time.perf_counter() - t0
     ok = bool(torch.equal(x, ref))  # fwd then inv is the identity: full-size self-check
     kern_ms = ev.total_ms()
-    return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L)
+    floor_ms = None
+    if L == 1:
+        # the compute floor of the same launches: rg_set_probe(4) swaps in the ntt16_pass variant
+        # with no HBM data loads / stores (butterflies, twiddle loads and LDS exchanges as in the
+        # production kernel), timed the same way; x is not written while the probe is set
+        lib = ringo.lib()
+        if hasattr(lib, "rg_set_probe") and lib.rg_set_probe(4) == 0:
+            try:
+                for _ in range(max(2, warmup)):
+                    step()
+                torch.cuda.synchronize()
+                evp = Events(torch, stream)
+                evp.start()
+                for _ in range(steps):
+                    step()
+                evp.stop()
+                torch.cuda.synchronize()
+                floor_ms = evp.total_ms() / steps
+            finally:
+                lib.rg_set_probe(0)
+            ok = ok and bool(torch.equal(x, ref))
+    return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L, compute_floor_ms=floor_ms)
 
 
 def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world, eval_steps=0):
@@ -330,7 +355,8 @@ def line_counters(C, line, units_per_step, kernel_ms_per_step):
         return None, None
     Lc = C["lines"][line]
     se = Lc.get("steps_executed") or {line: Lc["steps"]}
-    fetch = write = valu = 0.0
+    mix = VALU_MIX.get("kernels", {}) if VALU_MIX.get("lib_sha256") == C.get("lib_sha256") else {}
+    fetch = write = valu = cyc = 0.0
     for n, k in Lc["kernels"].items():
         if not any(p in n for p in LINE_KERNELS[line]):
             continue
@@ -339,14 +365,22 @@ def line_counters(C, line, units_per_step, kernel_ms_per_step):
             st += se.get(line + "_injected", 0)
         fetch += k.get("FETCH_SIZE", 0.0) / st  # KiB per step
         write += k.get("WRITE_SIZE", 0.0) / st
-        valu += k.get("SQ_INSTS_VALU", 0.0) / st
+        v = k.get("SQ_INSTS_VALU", 0.0) / st
+        valu += v
+        cyc += v * mix.get(n, {}).get("mean_cycles", VALU_CYCLES)
     traffic = (2.0 * fetch + write) * 1024.0 / units_per_step  # gfx950: FETCH_SIZE counts half
-    floor_ms = valu * VALU_CYCLES / (SIMDS * CLOCK_HZ) * 1e3
-    vb = {"insts_per_unit": valu / units_per_step, "cycles_per_inst": VALU_CYCLES, "simds": SIMDS,
+    floor_ms = cyc / (SIMDS * CLOCK_HZ) * 1e3
+    vb = {"insts_per_unit": valu / units_per_step, "cycles_per_inst": cyc / valu if valu else None, "simds": SIMDS,
           "clock_ghz": CLOCK_HZ / 1e9, "issue_floor_ms_per_step": floor_ms,
           "frac": floor_ms / kernel_ms_per_step if kernel_ms_per_step else None,
-          "note": "SQ_INSTS_VALU (wave64 instructions) x cycles/inst / (SIMDs x clock) = the VALU issue floor; "
-                  "frac = floor / measured time (how close this VALU-bound line runs to its instruction roof)"}
+          "cycle_model": ("per kernel: SQ_INSTS_VALU x the mean measured issue cost of its static VALU mix "
+                          "(profiles/valu_mix.json, tools/valu_mix.py; full-rate ops 2.4, half-rate 4.5, "
+                          "transcendental 9 cycles per wave64 instruction per SIMD)") if mix else
+                         f"uniform {VALU_CYCLES} cycles per instruction (no valu_mix.json for this library)",
+          "note": "issue floor = sum over kernels of VALU instructions x cycles / (SIMDs x clock); frac = floor / "
+                  "measured time.  Static per-class costs ignore dual issue of independent full/half-rate pairs, "
+                  "so this floor can sit above a kernel's true compute floor; where measured, "
+                  "compute_floor_ms_per_step (the kernel with its HBM traffic removed) is the direct figure"}
     return traffic, vb
 
 
@@ -630,6 +664,15 @@ def main():
         bytes_per_ntt = 2 * N * 8
         achieved = bytes_per_ntt * r["ntts"] / (kern_ms / 1000.0) / 1e9
         traffic, vb = line_counters(C, "ntt", 2 * args.batch, kern_ms / args.steps)
+        cf = r.get("compute_floor_ms")
+        if cf is not None:
+            cf = reduce_max(torch, dist, cf)
+            vb = dict(vb or {})
+            vb.update({"compute_floor_ms_per_step": cf, "compute_frac": cf / (kern_ms / args.steps),
+                       "compute_floor_note": "the same ntt16_pass launches with their HBM data loads and stores "
+                                             "removed (rg_set_probe(4): butterflies, twiddle loads, LDS exchanges "
+                                             "kept), HIP-event timed on the launch stream; compute_frac = that "
+                                             "time / the production step's kernel time"})
         out.update({
             "metric": "NTTs/sec (fwd+inv negacyclic, degree 2^16, 63-bit prime, batch 1024/GPU)",
             "value": world * 2 * args.batch / (ms_step / 1000.0),

@@ -380,6 +380,11 @@ rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream
 rg_status rg_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, void* stream);
 rg_status rg_stream_sync(void* stream);
 rg_status rg_set_device(int device);
+/* Measurement hook (bench.py's roofline block; not for production calls): probe 4 makes the
+ * single-word 2^16 NTT launches (ntt16_pass) skip their HBM data loads and stores, so the same
+ * launches time the kernel's compute floor (butterflies, twiddle loads, LDS exchanges); their
+ * outputs are then meaningless.  0 restores the production kernels.  Process-wide. */
+rg_status rg_set_probe(int probe);
 /* the calling thread's current device (one rank per GPU: LOCAL_RANK -> rg_set_device) */
 rg_status rg_get_device(int* device);
 rg_status rg_device_count(int* n);

@@ -13,6 +13,8 @@
 namespace rg {
 
 void set_last_error(const std::string& msg);
+// rg_set_probe: process-wide measurement probe (0 = production kernels)
+int measure_probe();
 
 #define RG_HIP(call)                                                                            \
   do {                                                                                          \

@@ -1463,6 +1463,9 @@ struct SampleArgs {
   // COSAC samples left unresolved by a phase of cosac_noise_kernel: a segment per wave
   unsigned long long* cos_seg;
   long long cos_cap;
+  // cdt2_noise_kernel's tail bounds: [129][size + 2], row c, entry j + 1 = the reference's tail
+  // cdf sum_{x = tailLo}^{j} rho(x - c/128) / norm for j = -1 .. size (host, Go's order)
+  const double* cdt_sbound;
 };
 
 // a TwinCDT sample whose two table searches disagree (twin_cdt.go:95-110): enc_noise[out]
@@ -1832,6 +1835,234 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
   }
   }
   if (lane == 0) a.tail_n[wv] = (int)ntail;
+}
+
+// ---- cdt2: TwinCDT for every encode polynomial, tails decided inline ----------------------
+// cdt_noise_kernel<true> spends its time on (round-2 profiling variants) the deltaInv centres,
+// 16 dependent global loads per polynomial, and eight table searches per lane; its v0 != v1
+// tails go to a second kernel that sums up to 2 tailHi + 1 exp terms each.  Here:
+//  * the polynomial's 256 digits are staged in a wave-private 1 KiB LDS slot (one 16-B store per
+//    lane), the next polynomial's digits already in flight, and the 16 shifted digit quadruples a
+//    lane needs are 16 independent ds_read_b128;
+//  * one search per sample (table c0: guide by top byte, bisection on the high words); table c1
+//    gives the same lower bound unless u lies between the two tables' entries around it (two
+//    word compares; ~0.1% of samples search c1 in full);
+//  * a v0 != v1 tail compares p = u / 2^64 with the reference's cdf = sum_{x <= v0} rho(x - cFrac)
+//    / norm through bounds: that sum decreases with the centre, cFrac lies in [c0, c0 + 1] / 128,
+//    so S[c0 + 1][v0] (1 - 2^-40) <= cdf <= S[c0][v0] (1 + 2^-40) (S summed on the host in the same
+//    order; 2^-40 covers both libms and the float sums).  Outside that band the comparison is
+//    decided; inside it (p within 1e-12 of the sum: p ~ 1, unseen in practice) the wave sums the
+//    terms in the reference's order, as cdt_noise_kernel does.  Results equal the reference's
+//    draw for draw; cdt_tail_kernel is not needed.
+constexpr int kCdt2Waves = 16;
+__host__ __device__ constexpr int cdt2_dig_off(int size) { return cdt_key_off(size) + kKeyWords * 4; }
+__host__ __device__ constexpr int cdt2_dyn_lds(int size) { return cdt2_dig_off(size) + kCdt2Waves * 1024; }
+
+__global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  extern __shared__ uint32_t dyn[];
+  const CdtDev& C = a.cdt_enc;
+  const int n = C.size;
+  uint32_t* thi = dyn;
+  uint8_t* guide = reinterpret_cast<uint8_t*>(dyn) + cdt_guide_off(n);
+  uint32_t* keyl = dyn + cdt_key_off(n) / 4;
+  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint4* dl = reinterpret_cast<uint4*>(reinterpret_cast<char*>(dyn) + cdt2_dig_off(n) + wl * 1024);
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(keyl, a.key[kDomEncCdt]);
+  for (int i = threadIdx.x; i < 128 * n; i += blockDim.x) thi[i] = (uint32_t)(C.tables[i] >> 32);
+  for (int i = threadIdx.x; i < 128 * 257; i += blockDim.x) guide[i] = C.guide[i];
+  __syncthreads();
+  const JShape& S = a.s;
+  const long long npoly = a.batch * (S.cols + 1) * S.rows;
+  const long long nw = (long long)gridDim.x * kCdt2Waves;
+  const double norm = sqrt(2.0 * M_PI) * C.sigma;
+  const double two_s2 = 2.0 * C.sigma * C.sigma;
+  const LdsKey key{keyl};
+  const int sstride = n + 2;
+  // u >= t[j] / u < t[j] on table `tab` (high word from LDS, full word on a tie)
+  auto ge = [&](int tab, int j, uint64_t u) {
+    const uint32_t th = thi[tab * n + j], uh = (uint32_t)(u >> 32);
+    return th != uh ? th > uh : C.tables[(long long)tab * n + j] >= u;
+  };
+  for (long long p0 = ((long long)blockIdx.x * kCdt2Waves + wl) * kCdtChunk; p0 < npoly; p0 += nw * kCdtChunk) {
+    const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
+    int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
+    uint4 gnext = reinterpret_cast<const uint4*>(a.digits + p0 * 256)[lane];
+    for (long long poly = p0; poly < p1; ++poly) {  // (b, col, row) flattened
+      if (poly > p0 && ++row == S.rows) {
+        row = 0;
+        if (++col == S.cols + 1) col = 0;
+      }
+      const uint4 g = gnext;
+      if (poly + 1 < p1) gnext = reinterpret_cast<const uint4*>(a.digits + (poly + 1) * 256)[lane];
+      long long* out = a.enc_noise + poly * 256;
+      if (enc_skipped(S, col, row)) {  // the reference draws nothing for these (prover.go:101-105,118-123)
+        reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(0, 0);
+        reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(0, 0);
+        continue;
+      }
+      const double sd =
+          col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
+      const bool cdt = sd == a.sd_ecd;
+      dl[lane] = g;
+      wave_lds_fence();
+      // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order):
+      // coefficient k reads digit (k + (i+1) slots) mod 256, added when that index wrapped
+      double fp[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int i = 0; i < S.exp; ++i) {
+        const double di = a.delta[i];
+        if (di == 0.0) continue;
+        const int base = 4 * lane + (i + 1) * S.slots;
+        const uint4 q = dl[(base & 255) >> 2];
+        const uint32_t gv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          if (base + h >= 256)
+            fp[h] = fp[h] + di * (double)gv[h];
+          else
+            fp[h] = fp[h] - di * (double)gv[h];
+        }
+      }
+      wave_lds_fence();  // the slot is rewritten for the next polynomial after these reads
+      if (!cdt) {  // a COSAC polynomial: hand the centres to cosac_noise_kernel
+        reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
+        reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
+        continue;
+      }
+      const unsigned long long gpoly =
+          a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
+      uint64_t u[4];
+      ks_words(key, gpoly, (uint64_t)(2 * lane), lds, u[0], u[1]);
+      ks_words(key, gpoly, (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
+      // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111)
+      int c0[4], c1[4], lo[4], len[4];
+      double cf[4], flo[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const double center = -fp[h];
+        flo[h] = floor(center);
+        cf[h] = center - flo[h];
+        c0[h] = (int)((int64_t)floor(128.0 * cf[h]) % 128);
+        c1[h] = (int)((int64_t)ceil(128.0 * cf[h]) % 128);
+        const int t = (int)(u[h] >> 56);
+        lo[h] = guide[c0[h] * 257 + t];
+        len[h] = guide[c0[h] * 257 + t + 1] - lo[h];  // lower_bound in [lo, lo + len]
+      }
+      for (;;) {  // bisection on table c0's high words (the full word on a tie)
+        bool more = false;
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if (len[h] > 0) {
+            const int half = len[h] >> 1;
+            if (!ge(c0[h], lo[h] + half, u[h])) {
+              lo[h] += half + 1;
+              len[h] -= half + 1;
+            } else {
+              len[h] = half;
+            }
+            more |= len[h] > 0;
+          }
+        if (!__ballot(more)) break;
+      }
+      int v0[4], v1[4];
+      uint32_t pend = 0, full1 = 0;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int lb = lo[h];
+        const bool e0 = lb < n && thi[c0[h] * n + lb] == (uint32_t)(u[h] >> 32) && C.tables[(long long)c0[h] * n + lb] == u[h];
+        v0[h] = lb - (e0 ? 1 : 0);
+        if (c1[h] == c0[h]) {
+          v1[h] = v0[h];
+        } else if ((lb == n || ge(c1[h], lb, u[h])) && (lb == 0 || !ge(c1[h], lb - 1, u[h]))) {
+          const bool e1 = lb < n && thi[c1[h] * n + lb] == (uint32_t)(u[h] >> 32) &&
+                          C.tables[(long long)c1[h] * n + lb] == u[h];
+          v1[h] = lb - (e1 ? 1 : 0);  // table c1 has the same lower bound
+        } else {
+          full1 |= 1u << h;
+        }
+      }
+      if (__ballot(full1 != 0)) {  // rare: a full search of table c1
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          lo[h] = 0;
+          len[h] = (full1 >> h) & 1 ? n : 0;
+        }
+        for (;;) {
+          bool more = false;
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            if (len[h] > 0) {
+              const int half = len[h] >> 1;
+              if (!ge(c1[h], lo[h] + half, u[h])) {
+                lo[h] += half + 1;
+                len[h] -= half + 1;
+              } else {
+                len[h] = half;
+              }
+              more |= len[h] > 0;
+            }
+          if (!__ballot(more)) break;
+        }
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if ((full1 >> h) & 1) {
+            const int lb = lo[h];
+            const bool e1 = lb < n && C.tables[(long long)c1[h] * n + lb] == u[h];
+            v1[h] = lb - (e1 ? 1 : 0);
+          }
+      }
+      int64_t res[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        res[h] = (int64_t)v1[h] + C.tail_lo + (int64_t)flo[h];
+        if (v0[h] != v1[h]) {  // the tail: p < cdf -> v0's value (twin_cdt.go:95-110)
+          const double p = __ull2double_rn(u[h]) / 18446744073709551616.0;
+          const double lo_b = a.cdt_sbound[(c0[h] + 1) * sstride + v0[h] + 1] * (1.0 - 9.094947017729282e-13);
+          const double hi_b = a.cdt_sbound[c0[h] * sstride + v0[h] + 1] * (1.0 + 9.094947017729282e-13);
+          if (p < lo_b)
+            res[h] = (int64_t)v0[h] + C.tail_lo + (int64_t)flo[h];
+          else if (!(p >= hi_b))
+            pend |= 1u << h;  // within the bounds' band: sum the terms below
+        }
+      }
+#if RG_VAR & 1
+      pend = 0;
+#endif
+      for (;;) {  // the exact sums (p within ~1e-12 of the cdf), one sample at a time across the wave
+        const uint64_t any = __ballot(pend != 0);
+        if (!any) break;
+        const int src = __builtin_amdgcn_readfirstlane(__builtin_ctzll(any));
+        const int hs = __builtin_amdgcn_readlane(pend ? __builtin_ctz(pend) : 0, src);
+        double c_frac = 0.0, p = 0.0;
+        int vv = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if (h == hs) {
+            c_frac = cf[h];
+            vv = v0[h];
+            p = __ull2double_rn(u[h]) / 18446744073709551616.0;
+          }
+        c_frac = rl_f64(c_frac, src);
+        vv = __builtin_amdgcn_readlane(vv, src);
+        double cdf = 0.0;
+        for (int64_t x0 = C.tail_lo; x0 <= vv; x0 += 64) {
+          const double xf = (double)(x0 + lane);
+          const double term = exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm;
+          const int nn = (int)std::min<int64_t>(64, (int64_t)vv - x0 + 1);
+          for (int i = 0; i < nn; ++i) cdf += rl_f64(term, i);
+        }
+        if (lane == src) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            if (h == hs && p < cdf) res[h] = (int64_t)v0[h] + C.tail_lo + (int64_t)flo[h];
+          pend &= pend - 1;
+        }
+      }
+      reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(res[0], res[1]);
+      reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(res[2], res[3]);
+    }
+  }
 }
 
 // The deferred TwinCDT tails: wave w resolves segment w, two entries at a time (32 lanes each):
@@ -2228,6 +2459,241 @@ __global__ __launch_bounds__(kCosacThreads) void cosac_noise_kernel(SampleArgs a
 }
 #pragma clang fp contract(on)
 
+// ---- cosac2: every COSAC sample through one state machine, one AES block per lane per step ----
+// cosac_noise_kernel precomputes 3 / 5 / 7 keystream blocks per sample in lockstep phases and
+// recomputes them from scratch for the samples a phase leaves open (~5 blocks per sample against
+// the ~3.7 that per-sample instances need), with 236 VGPRs (2 waves per SIMD: the AES lookups'
+// LDS latency is exposed).  Here each wave's samples (its jobs' 256 coefficients each, in order)
+// form a queue; a lane takes the next sample when its current one is done, and every iteration
+//   1. lets each lane consume its buffered word (the second word of its stream's last block)
+//      while the state machine wants a word it has, then
+//   2. computes ONE AES block per lane: the next block of whichever stream (the sampler's own
+//      instance or its rounded sampler's) the lane's state needs, keys selected per lane from LDS,
+//      and consumes its first word.
+// So every lane with work computes a useful block on every iteration; the words drawn are those
+// of cosac_noise_kernel (same instances, same order), so the outputs are identical.  The lane
+// state is kept small (x / u / y share a register: each is live in disjoint states).
+constexpr int kCos2Threads = 1024;
+constexpr int kCos2KeyStride = kKeyWords + 4;  // keys of the two streams 4 banks apart
+
+struct Cos2Lane {
+  int g;                // queue index of the current sample, -1: none
+  int st;               // state | zi << 8 | zb << 15 | code << 16
+  unsigned long long oi;  // enc_noise index
+  uint32_t pos[2];      // next word of each stream's instance
+  uint32_t have;        // bit s: spare[s] holds word pos[s]
+  uint64_t spare[2];
+  double c_int, c_frac, t, y_round;  // t: x (wedge), u (tail), y (bit / rr)
+};
+
+template <class Z>
+__device__ __forceinline__ void cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, const double* sdv, long long* en) {
+  const double rn = 3.442619855899;
+  const int st = L.st & 255, code = L.st >> 16;
+  const double sd = sdv[4 * code], two_s2 = sdv[4 * code + 1], lead = sdv[4 * code + 2], inv_lead = sdv[4 * code + 3];
+  const double fw = float52(w);
+  double arg = 0.0;
+  bool need_e = false, acc = false;
+  if (st == kCoStart) {
+    arg = -(L.c_frac * L.c_frac) / two_s2;
+    need_e = fw < inv_lead;
+  }
+  if (st == kCoWedge) {
+    arg = -0.5 * L.t * L.t;
+    need_e = true;
+  }
+  if (st == kCoRR) {
+    arg = -((L.y_round + L.c_frac) * (L.y_round + L.c_frac) - L.t * L.t) / two_s2;
+    acc = arg >= 0.0 || fw < (1.0 + arg) * 0.99999999999999644729;
+    need_e = !acc;
+  }
+  double e = 0.0, lg = 0.0;
+  if (need_e) e = exp(arg);
+  if (st == kCoTailU || st == kCoTailV) lg = -log(fw);
+  double nf = 0.0;
+  bool have_nf = false;
+  int nst = st;
+  switch (st) {
+    case kCoStart:  // gaussian_cosac.go:36-40
+      if (need_e && fw < e / lead) {
+        en[L.oi] = (long long)L.c_int;
+        L.g = -1;
+      } else {
+        nst = kCoNorm;
+      }
+      break;
+    case kCoNorm: {  // gaussian_rounded.go:80-92
+      const uint64_t b = w >> 63;
+      const uint32_t i = (uint32_t)(w & 127u);
+      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
+      const double x = (double)(int64_t)((j ^ (0ull - b)) + b) * Zg.wn[i];
+      if (j < Zg.kn[i]) {
+        nf = x;
+        have_nf = true;
+      } else if (i == 0) {
+        L.st = (L.st & ~(1 << 15)) | ((int)b << 15);
+        nst = kCoTailU;
+      } else {
+        L.st = (L.st & ~(127 << 8)) | ((int)i << 8);
+        L.t = x;
+        nst = kCoWedge;
+      }
+      break;
+    }
+    case kCoTailU:  // gaussian_rounded.go:94-101
+      L.t = lg * (1.0 / rn);
+      nst = kCoTailV;
+      break;
+    case kCoTailV:
+      if (lg + lg >= L.t * L.t) {
+        const double uu = L.t + rn;
+        nf = ((L.st >> 15) & 1) ? -uu : uu;
+        have_nf = true;
+      } else {
+        nst = kCoTailU;
+      }
+      break;
+    case kCoWedge: {  // gaussian_rounded.go:109-113
+      const int zi = (L.st >> 8) & 127;
+      const double f0 = Zg.fn[zi - 1], f1 = Zg.fn[zi];
+      if (fw * (f0 - f1) < e - f1) {
+        nf = L.t;
+        have_nf = true;
+      } else {
+        nst = kCoNorm;
+      }
+      break;
+    }
+    case kCoBit: {  // gaussian_cosac.go:43-50
+      bool cmp;
+      if ((w & 1) == 0) {
+        L.y_round = round(L.t) - 1.0;
+        cmp = L.y_round <= 0.5;
+      } else {
+        L.y_round = round(L.t) + 1.0;
+        cmp = L.y_round >= -0.5;
+      }
+      nst = cmp ? kCoRR : kCoNorm;
+      break;
+    }
+    default:  // kCoRR, gaussian_cosac.go:51-55
+      if (acc || fw < e) {
+        en[L.oi] = (long long)L.y_round + (long long)L.c_int;
+        L.g = -1;
+      } else {
+        nst = kCoNorm;
+      }
+      break;
+  }
+  if (have_nf) {
+    L.t = sd * nf;
+    nst = kCoBit;
+  }
+  L.st = (L.st & ~255) | nst;
+}
+
+__global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArgs a) {
+  __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t keys[2 * kCos2KeyStride];
+  __shared__ uint64_t zig[384];  // kn, wn, fn
+  __shared__ double sdv[12];     // per sd code: sd, 2 sd^2, sqrt(2 pi) sd, 1 / that
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(keys, a.key[kDomCosac]);
+  aes_key_fill(keys + kCos2KeyStride, a.key[kDomCosacRnd]);
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    zig[i] = a.zig.kn[i];
+    zig[128 + i] = __double_as_longlong(a.zig.wn[i]);
+    zig[256 + i] = __double_as_longlong(a.zig.fn[i]);
+  }
+  if (threadIdx.x < 3) {
+    const double sd = threadIdx.x == 0 ? a.sd_ecd_blind : threadIdx.x == 1 ? a.sd_mask : a.sd_mask_blind;
+    const double lead = sqrt(2.0 * M_PI) * sd;
+    sdv[4 * threadIdx.x] = sd;
+    sdv[4 * threadIdx.x + 1] = 2.0 * sd * sd;
+    sdv[4 * threadIdx.x + 2] = lead;
+    sdv[4 * threadIdx.x + 3] = 1.0 / lead;
+  }
+  __syncthreads();
+  const ZigDev Z{zig, reinterpret_cast<const double*>(zig + 128), reinterpret_cast<const double*>(zig + 256)};
+  const JShape& S = a.s;
+  const int lane = threadIdx.x & 63;
+  const long long nwaves = (long long)gridDim.x * (kCos2Threads / 64);
+  const long long wid = (long long)blockIdx.x * (kCos2Threads / 64) + (threadIdx.x >> 6);
+  const int per = S.cols + S.rows;
+  const long long njobs = a.batch * per;
+  const long long myjobs = njobs > wid ? (njobs - wid + nwaves - 1) / nwaves : 0;
+  const long long total = myjobs * 256;  // this wave's queue
+  const unsigned long long pb256 = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * 256ull;
+  auto mb = [](uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  };
+  Cos2Lane L;
+  L.g = -1;
+  L.st = 0;
+  long long next = 0;
+  for (;;) {
+    bool can = L.g >= 0 && ((L.have >> co_src(L.st & 255)) & 1);
+    uint64_t w = 0;
+    if (!__ballot(can)) {
+      // no lane can step on a buffered word: lanes without a sample take the next ones of the
+      // queue (samples of jobs that draw nothing are dropped here), then every lane with work
+      // computes the next block of the stream its state needs and steps on its first word
+      for (;;) {
+        const uint64_t need = __ballot(L.g < 0);
+        if (!need || next >= total) break;
+        const int rank = mb(need);
+        if (L.g < 0 && next + rank < total) {
+          const long long g = next + rank;
+          const long long job = wid + (g >> 8) * nwaves;
+          const long long b = job / per;
+          const int j = (int)(job % per);
+          const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
+          const int code = col < S.cols ? 0 : (row == 0 ? 2 : 1);
+          if (!enc_skipped(S, col, row) && sdv[4 * code] != a.sd_ecd) {
+            L.g = (int)g;
+            L.oi = (unsigned long long)(((b * (S.cols + 1) + col) * S.rows + row) * 256 + (g & 255));
+            const double center = __longlong_as_double(a.enc_noise[L.oi]);
+            L.c_int = round(center);
+            L.c_frac = L.c_int - center;
+            L.st = kCoStart | (code << 16);
+            L.pos[0] = L.pos[1] = 0;
+            L.have = 0;
+          }
+        }
+        next += __builtin_popcountll(need);
+      }
+      if (!__ballot(L.g >= 0)) break;
+      if (L.g >= 0) {
+        const int s = co_src(L.st & 255);
+        const uint32_t p = L.pos[s];
+        const LdsKey k{keys + s * kCos2KeyStride};
+        const unsigned long long inst = pb256 + L.oi;
+        if (p < 1024) {
+          uint64_t w1;
+          ks_words(k, inst, p / 2, lds, w, w1);
+          if (s)
+            L.spare[1] = w1;
+          else
+            L.spare[0] = w1;
+        } else {  // past the first 8 KiB buffer: the XOR-accumulated refill (rare)
+          w = uniform_word_at(k, lds, inst, p);
+        }
+        // spare[s] is word p + 1, the stream's next word once the step below has taken word p
+        L.have = p < 1024 ? (L.have | (1u << s)) : (L.have & ~(1u << s));
+        can = true;
+      }
+    } else if (can) {
+      const int s = co_src(L.st & 255);
+      w = s ? L.spare[1] : L.spare[0];
+      L.have &= ~(1u << s);
+    }
+    if (can) {
+      ++L.pos[co_src(L.st & 255)];
+      cos2_step(L, w, Z, sdv, a.enc_noise);
+    }
+  }
+}
+
 // thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
 __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
@@ -2575,7 +3041,7 @@ struct rg_jindo_scratch {
 struct rg_jindo_samplers {
   bool ready = false;
   double sd[6];  // ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe
-  rg::DevBuf te0, cdt_enc, cdt_guide, cdt_mlwe, zig, delta;
+  rg::DevBuf te0, cdt_enc, cdt_guide, cdt_sbound, cdt_mlwe, zig, delta;
   int cdt_enc_size = 0, cdt_mlwe_size = 0;
   int64_t tail_lo_enc = 0, tail_lo_mlwe = 0;
   std::vector<double> h_delta;
@@ -3169,6 +3635,16 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     }
     a.tails = sc->tails.as<CdtTail>();
     a.tail_n = sc->tail_n.as<int>();
+    a.cdt_sbound = S.cdt_sbound.as<double>();
+    static const bool cdt_legacy = [] {  // RINGO_CDT=legacy: cdt_noise_kernel + cdt_tail_kernel (A/B)
+      const char* e = getenv("RINGO_CDT");
+      return e && e[0] == 'l';
+    }();
+    if (!cdt_legacy && S.cdt_enc_size <= kCdtLdsMaxSize && p.slots % 4 == 0 &&
+        cdt2_dyn_lds(S.cdt_enc_size) + (int)sizeof(uint32_t) * kAesLds <= 163840) {
+      hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
+      RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
+    } else {
     if (S.cdt_enc_size <= kCdtLdsMaxSize)
       hipLaunchKernelGGL(cdt_noise_kernel<true>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(true, S.cdt_enc_size), st, a);
     else
@@ -3176,6 +3652,7 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
     hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)nw), dim3(64 * kTailWavesPerSeg), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT tails)"));
+    }
     const long long ncos = (long long)batch * (p.cols + p.rows);  // jobs
     const long long wpb = kCosacThreads / 64;
     const unsigned gc = (unsigned)std::min<long long>((ncos + wpb - 1) / wpb, 1024);
@@ -3187,7 +3664,17 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
       RG_TRY(sc->cos_seg.alloc(cb));
     }
     a.cos_seg = sc->cos_seg.as<unsigned long long>();
-    hipLaunchKernelGGL(cosac_noise_kernel, dim3(gc), dim3(kCosacThreads), 0, st, a);
+    static const bool cos_legacy = [] {  // RINGO_COSAC=legacy: the three-phase cosac_noise_kernel (A/B)
+      const char* e = getenv("RINGO_COSAC");
+      return e && e[0] == 'l';
+    }();
+    if (cos_legacy) {
+      hipLaunchKernelGGL(cosac_noise_kernel, dim3(gc), dim3(kCosacThreads), 0, st, a);
+    } else {
+      const long long w2 = kCos2Threads / 64;
+      const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
+      hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
+    }
     RG_TRY(check_launch("jindo enc noise (COSAC)"));
   } else {
     hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 511) / 512)), dim3(512), 0, st, a);
@@ -3856,6 +4343,24 @@ rg_status rg_jindo_set_stddevs(rg_jindo* J, const rg_jindo_stddevs* sd) {
       }
     }
     RG_TRY(S.cdt_guide.upload(guide.data(), guide.size()));
+  }
+  {  // cdt2's tail bounds: the reference's tail cdf (twin_cdt.go:101-105) at centres c / 128, c = 0..128
+    const int n = S.cdt_enc_size;
+    const double sigma = v[0], norm = std::sqrt(2.0 * M_PI) * sigma;
+    std::vector<double> sb((size_t)129 * (n + 2));
+    for (int c = 0; c <= 128; ++c) {
+      const double cf = (double)c / 128.0;
+      double cdf = 0.0;
+      int64_t x = S.tail_lo_enc;
+      for (int j = -1; j <= n; ++j) {  // entry j + 1: sum over x = tailLo .. j
+        for (; x <= j; ++x) {
+          const double xf = (double)x;
+          cdf += std::exp(-(xf - cf) * (xf - cf) / (2.0 * sigma * sigma)) / norm;
+        }
+        sb[(size_t)c * (n + 2) + j + 1] = cdf;
+      }
+    }
+    RG_TRY(S.cdt_sbound.upload(sb.data(), sb.size() * 8));
   }
   RG_TRY(S.cdt_mlwe.upload(ml.data(), ml.size() * 8));
   const Ziggurat Z = make_ziggurat();

@@ -254,7 +254,10 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 }
 
 // PROBE (tuning only; production = 0): 1 = twiddles from registers (no table loads),
-// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both
+// 2 = butterflies replaced by one add (memory / LDS / twiddle-load floor), 3 = both,
+// 4 = no global data loads / stores (the tile is synthesised from the thread index and its
+// result kept live by a store that never fires): the compute floor (butterflies, twiddle loads,
+// LDS exchanges) of the same launch, timed by bench.py through rg_set_probe
 template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
                                             uint32_t hi, uint32_t t) {
@@ -355,7 +358,10 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
   // ---- global load
-  if constexpr (COL) {
+  if constexpr ((PROBE & 4) != 0) {
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = (uint64_t)(tid * 0x9E3779B9u + tile * 8u + (uint32_t)y);
+  } else if constexpr (COL) {
     if constexpr (!INV) {
       const uint32_t vo = ((t << 8) + s) * 8u;
 #pragma unroll
@@ -370,6 +376,14 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
   }
+  // PROBE & 4: the result stays live through a store that never fires (values are < 2q < 2^64 - 1)
+  auto st64 = [&](uint64_t x, uint32_t voff, uint32_t soff) {
+    if constexpr ((PROBE & 4) != 0) {
+      if (x == ~0ull) rg_bstore(x, rout, voff, soff);
+    } else {
+      rg_bstore(x, rout, voff, soff);
+    }
+  };
   const uint32_t bH = 16 * t + s + 16 * (t >> 3), bM = s + 16 * (t & 3) + 576 * (t >> 2), bL = 144 * t + s;
   auto offM = [](int y) { return 64 * y + 16 * (y >> 1); };
   const uint32_t rH = 288 * s + t, rM = 288 * s + 36 * (t >> 2) + (t & 3), rL9 = 288 * s + 9 * t,
@@ -398,7 +412,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     if constexpr (COL) {
       const uint32_t vo = ((t << 11) + s) * 8u;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) rg_bstore(e[r], rout, vo, (uint32_t)r << 11);
+      for (int r = 0; r < 8; ++r) st64(e[r], vo, (uint32_t)r << 11);
     } else {  // L -> H through LDS (pad x >> 5), then coalesced rows
       __syncthreads();
 #pragma unroll
@@ -406,7 +420,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
       __syncthreads();
       const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) rg_bstore(lds[rH + 33 * y], rout, vo + 256u * y, 0);
+      for (int y = 0; y < 8; ++y) st64(lds[rH + 33 * y], vo + 256u * y, 0);
     }
   } else {
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
@@ -440,11 +454,11 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     if constexpr (COL) {
       const uint32_t vo = ((t << 8) + s) * 8u;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo, (uint32_t)y << 16);
+      for (int y = 0; y < 8; ++y) st64(e[y], vo, (uint32_t)y << 16);
     } else {
       const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) rg_bstore(e[y], rout, vo + 256u * y, 0);
+      for (int y = 0; y < 8; ++y) st64(e[y], vo + 256u * y, 0);
     }
   }
 }

@@ -23,6 +23,13 @@ static bool lazy_disabled() {
 template <bool INV, bool COL, bool SCALE, bool CANON>
 static rg_status launch64(const Ntt64Args& a, size_t polys, hipStream_t st) {
   const long long tiles = a.total_sub / 16;
+  if (measure_probe() == 4) {  // bench.py's compute-floor measurement (rg_set_probe): no HBM data movement
+    if (!COL && polys % 16 == 0)
+      hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, true, 1, 4>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, false, 1, 4>), dim3((unsigned)tiles), dim3(512), 0, st, a);
+    return check_launch("ntt16_pass (probe)");
+  }
   if (!COL && polys % 16 == 0)
     hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, true>), dim3((unsigned)tiles), dim3(512), 0, st, a);
   else

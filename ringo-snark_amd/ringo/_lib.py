@@ -120,6 +120,7 @@ _SIGS = {
     "rg_stream_sync": (ctypes.c_int, [vp]),
     "rg_set_device": (ctypes.c_int, [ctypes.c_int]),
     "rg_get_device": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "rg_set_probe": (ctypes.c_int, [ctypes.c_int]),
     "rg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
 }
 

@@ -183,8 +183,8 @@ def test_first_commit_range_rejected():
     q = int(P["field_q_hex"], 16)
     params = jindo.Parameters.from_dict(P, q)
     prv = jindo.NewProver(params, b"Jindo!")
-    per = (P["cols"] + 1) * P["rows"] * P["d"]  # the largest per-commit instance count here
-    assert per >= (P["cols"] + 1) * (P["in_msis"] + P["mlwe"]) * P["d"]
+    per = max((P["cols"] + 1) * P["rows"] * P["d"], (P["cols"] + 1) * (P["in_msis"] + P["mlwe"]) * P["d"],
+              (P["cols"] + P["rows"]) * P["slots"])  # the largest per-commit instance count of a domain
     v = make_v(q, 64, seed=5)[None]
     sh = params.shapes(1)
     o = {k: torch.zeros(sh[k], dtype=torch.int64, device="cuda") for k in ("last_row", "mask", "enc_noise", "mlwe_noise")}
