@@ -1589,12 +1589,13 @@ int of_jindo_sample(const of_jindo* J, const double* sd, const double* delta, co
           of_uni U;
           uni_init(&U, &dom[0], gpoly);
           for (int k = 0; k < d; ++k) en[k] = cdt_sample(&ce, &U, -fp[k]);
-        } else {
-          for (int k = 0; k < d; ++k) { /* cosac: an instance per sample for each of its streams */
+        } else { /* cosac: an instance pair per group of G consecutive samples, drawn in order */
+          const int G = d < 16 ? d : 16;
+          for (int g = 0; g < d / G; ++g) {
             of_uni B, R;
-            uni_init(&B, &dom[1], gpoly * d + k);
-            uni_init(&R, &dom[2], gpoly * d + k);
-            en[k] = cosac_sample(&B, &R, -fp[k], s);
+            uni_init(&B, &dom[1], gpoly * (uint64_t)(d / G) + (uint64_t)g);
+            uni_init(&R, &dom[2], gpoly * (uint64_t)(d / G) + (uint64_t)g);
+            for (int k = g * G; k < (g + 1) * G; ++k) en[k] = cosac_sample(&B, &R, -fp[k], s);
           }
         }
       }

@@ -1430,8 +1430,8 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
 // device, from six sampler domains (csprng.hpp: one AES-256-CTR key per domain, a window of
 // the domain's counter space per sampler instance):
 //   kDomEncCdt    Encoder.twinCDT      one instance per encode polynomial (256 words)
-//   kDomCosac     Encoder.cosac        one instance per sample ...
-//   kDomCosacRnd  ... and its RoundedGaussianSampler, one instance per sample
+//   kDomCosac     Encoder.cosac        one instance per group of kCosGroup samples (in order) ...
+//   kDomCosacRnd  ... and its RoundedGaussianSampler, the same groups
 //   kDomMlweCdt   Prover.mlweSampler   one instance per MLWE polynomial
 //   kDomMlweRnd   Prover.roundedSampler one instance per sample
 //   kDomUniform   crypto/rand (MustSetRandom), one instance per field element
@@ -1439,6 +1439,7 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
 // prover's sequence, so batches and ranks never share keystream.
 // ------------------------------------------------------------------------------------------
 enum { kDomEncCdt = 0, kDomCosac, kDomCosacRnd, kDomMlweCdt, kDomMlweRnd, kDomUniform, kNumDom };
+constexpr int kCosGroup = 16;  // COSAC samples per sampler-instance pair (d >= 16; d < 16: d)
 
 struct SampleArgs {
   JShape s;
@@ -1460,12 +1461,10 @@ struct SampleArgs {
   struct CdtTail* tails;
   int* tail_n;
   long long tail_cap;
-  // COSAC samples left unresolved by a phase of cosac_noise_kernel: a segment per wave
-  unsigned long long* cos_seg;
-  long long cos_cap;
   // cdt2_noise_kernel's tail bounds: [129][size + 2], row c, entry j + 1 = the reference's tail
   // cdf sum_{x = tailLo}^{j} rho(x - c/128) / norm for j = -1 .. size (host, Go's order)
   const double* cdt_sbound;
+  const int* cdt_jmax;  // [128]: v0 <= jmax[c0] decides the sample as v0 (cdt2_noise_kernel)
 };
 
 // a TwinCDT sample whose two table searches disagree (twin_cdt.go:95-110): enc_noise[out]
@@ -1525,13 +1524,13 @@ __global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
     ks_words(a.key[kDomEncCdt], gpoly, (uint64_t)m, lds, w0, w1);
     out[2 * m] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m), w0);
     out[2 * m + 1] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m + 1), w1);
-  } else {  // Encoder.cosac (encoder.go:171-172)
-    for (int h = 0; h < 2; ++h) {
-      const int k = 2 * m + h;
+  } else {  // Encoder.cosac (encoder.go:171-172): thread m < d / G draws group m's G samples in order
+    const int G = S.d < kCosGroup ? S.d : kCosGroup;
+    if (m < S.d / G) {
       Uniform base, rnd;
-      base.init(keys[0], lds, gpoly * S.d + k);
-      rnd.init(keys[1], lds, gpoly * S.d + k);
-      out[k] = cosac(a.zig, base, rnd, enc_centre(a, dg, k), sd);
+      base.init(keys[0], lds, gpoly * (unsigned long long)(S.d / G) + (unsigned long long)m);
+      rnd.init(keys[1], lds, gpoly * (unsigned long long)(S.d / G) + (unsigned long long)m);
+      for (int k = m * G; k < (m + 1) * G; ++k) out[k] = cosac(a.zig, base, rnd, enc_centre(a, dg, k), sd);
     }
   }
 }
@@ -1540,15 +1539,13 @@ __global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
 // enc_noise_kernel above runs both samplers in one grid and every sample's slow path inline,
 // so a wave waits for its slowest lane: the TwinCDT exp tail (v0 != v1: ~1/128 of samples, up
 // to |tail_lo| + v0 + 1 exp terms) and COSAC's rejection loop (max over 64 lanes of a ~50%
-// acceptance geometric).  The two kernels below draw the same words from the same instances,
-// so their output is identical:
-//   cdt_noise_kernel    wave per TwinCDT polynomial, 4 coefficients per lane (2 AES blocks);
-//                       the deltaInv centres from 16-byte digit loads; the 128
-//                       tables' high words in LDS (full words from global only on a tie);
-//                       tail samples resolved one at a time by the whole wave (lanes compute
-//                       the exp terms, then the sum in the reference's order via readlane).
-//   cosac_noise_kernel  wave per COSAC polynomial (row 0 and the mask column), the 256 samples
-//                       a queue that lanes refill as they accept (COSAC as a state machine).
+// acceptance geometric).  The kernels below draw the same words from the same instances, so
+// their output is identical:
+//   cdt2_noise_kernel   wave per TwinCDT polynomial, 4 coefficients per lane (2 AES blocks);
+//                       digits staged in LDS for the deltaInv centres; one guide-table lookup
+//                       per sample (cdt_noise_kernel + cdt_tail_kernel: the round-2 form, kept
+//                       behind RINGO_CDT=legacy);
+//   cosac2_noise_kernel COSAC groups as a work queue through one state machine.
 #ifndef RG_VAR
 #define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC)
 #endif
@@ -1655,7 +1652,7 @@ __host__ __device__ constexpr int cdt_dyn_lds(bool lds_table, int size) {
 
 // Each wave owns a contiguous range of the batch's (commit, column, row) polynomials: TwinCDT
 // polynomials are sampled; COSAC ones get their deltaInv centres (as doubles, in enc_noise)
-// for cosac_noise_kernel; skipped ones are zeroed.
+// for cosac2_noise_kernel; skipped ones are zeroed.
 template <bool LdsTable>
 __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
@@ -1717,7 +1714,7 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
           fp[h] = fp[h] - di * (double)gv[h];
       }
     }
-    if (!cdt) {  // a COSAC polynomial: hand the centres to cosac_noise_kernel
+    if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
       reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
       reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
       continue;
@@ -1856,7 +1853,8 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
 //    draw for draw; cdt_tail_kernel is not needed.
 constexpr int kCdt2Waves = 16;
 __host__ __device__ constexpr int cdt2_dig_off(int size) { return cdt_key_off(size) + kKeyWords * 4; }
-__host__ __device__ constexpr int cdt2_dyn_lds(int size) { return cdt2_dig_off(size) + kCdt2Waves * 1024; }
+__host__ __device__ constexpr int cdt2_jmax_off(int size) { return cdt2_dig_off(size) + kCdt2Waves * 1024; }
+__host__ __device__ constexpr int cdt2_dyn_lds(int size) { return cdt2_jmax_off(size) + 128 * 4; }
 
 __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
@@ -1868,10 +1866,12 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   uint32_t* keyl = dyn + cdt_key_off(n) / 4;
   const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint4* dl = reinterpret_cast<uint4*>(reinterpret_cast<char*>(dyn) + cdt2_dig_off(n) + wl * 1024);
+  int* jmax = reinterpret_cast<int*>(reinterpret_cast<char*>(dyn) + cdt2_jmax_off(n));
   aes_lds_fill(lds, a.te0);
   aes_key_fill(keyl, a.key[kDomEncCdt]);
   for (int i = threadIdx.x; i < 128 * n; i += blockDim.x) thi[i] = (uint32_t)(C.tables[i] >> 32);
   for (int i = threadIdx.x; i < 128 * 257; i += blockDim.x) guide[i] = C.guide[i];
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) jmax[i] = a.cdt_jmax[i];
   __syncthreads();
   const JShape& S = a.s;
   const long long npoly = a.batch * (S.cols + 1) * S.rows;
@@ -1880,11 +1880,6 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   const double two_s2 = 2.0 * C.sigma * C.sigma;
   const LdsKey key{keyl};
   const int sstride = n + 2;
-  // u >= t[j] / u < t[j] on table `tab` (high word from LDS, full word on a tie)
-  auto ge = [&](int tab, int j, uint64_t u) {
-    const uint32_t th = thi[tab * n + j], uh = (uint32_t)(u >> 32);
-    return th != uh ? th > uh : C.tables[(long long)tab * n + j] >= u;
-  };
   for (long long p0 = ((long long)blockIdx.x * kCdt2Waves + wl) * kCdtChunk; p0 < npoly; p0 += nw * kCdtChunk) {
     const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
     int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
@@ -1925,7 +1920,7 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
         }
       }
       wave_lds_fence();  // the slot is rewritten for the next polynomial after these reads
-      if (!cdt) {  // a COSAC polynomial: hand the centres to cosac_noise_kernel
+      if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
         reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
         reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
         continue;
@@ -1935,96 +1930,62 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       uint64_t u[4];
       ks_words(key, gpoly, (uint64_t)(2 * lane), lds, u[0], u[1]);
       ks_words(key, gpoly, (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
-      // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111)
-      int c0[4], c1[4], lo[4], len[4];
+      // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111).  Fast path: the guide bucket of u's
+      // top byte in table c0 holds <= 3 entries and none shares u's high word, so the lower bound
+      // is lo + #(entries below u) with no equality (three LDS word compares); and v0 <= jmax[c0],
+      // for which the reference returns v0 whatever v1 is: if v1 == v0 trivially, else because
+      // p = u / 2^64 <= t_c0[v0 + 1] / 2^64 < (1 - 2^-40) S[c0 + 1][v0] <= the cdf it compares
+      // with (host-checked per table and index, rg_jindo_set_stddevs).  Other samples (a long
+      // bucket, a high-word tie, an extreme v0) take the exact path below.
+      int c0[4], v0[4];
       double cf[4], flo[4];
+      uint32_t slow = 0;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         const double center = -fp[h];
         flo[h] = floor(center);
         cf[h] = center - flo[h];
         c0[h] = (int)((int64_t)floor(128.0 * cf[h]) % 128);
-        c1[h] = (int)((int64_t)ceil(128.0 * cf[h]) % 128);
         const int t = (int)(u[h] >> 56);
-        lo[h] = guide[c0[h] * 257 + t];
-        len[h] = guide[c0[h] * 257 + t + 1] - lo[h];  // lower_bound in [lo, lo + len]
-      }
-      for (;;) {  // bisection on table c0's high words (the full word on a tie)
-        bool more = false;
+        const int lo = guide[c0[h] * 257 + t];
+        const int len = guide[c0[h] * 257 + t + 1] - lo;
+        const uint32_t uh = (uint32_t)(u[h] >> 32);
+        const uint32_t* th = thi + c0[h] * n + lo;
+        int cnt = 0;
+        bool tie = false;
 #pragma unroll
-        for (int h = 0; h < 4; ++h)
-          if (len[h] > 0) {
-            const int half = len[h] >> 1;
-            if (!ge(c0[h], lo[h] + half, u[h])) {
-              lo[h] += half + 1;
-              len[h] -= half + 1;
-            } else {
-              len[h] = half;
-            }
-            more |= len[h] > 0;
+        for (int k = 0; k < 3; ++k)
+          if (k < len) {
+            const uint32_t x = th[k];
+            cnt += x < uh ? 1 : 0;
+            tie |= x == uh;
           }
-        if (!__ballot(more)) break;
-      }
-      int v0[4], v1[4];
-      uint32_t pend = 0, full1 = 0;
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const int lb = lo[h];
-        const bool e0 = lb < n && thi[c0[h] * n + lb] == (uint32_t)(u[h] >> 32) && C.tables[(long long)c0[h] * n + lb] == u[h];
-        v0[h] = lb - (e0 ? 1 : 0);
-        if (c1[h] == c0[h]) {
-          v1[h] = v0[h];
-        } else if ((lb == n || ge(c1[h], lb, u[h])) && (lb == 0 || !ge(c1[h], lb - 1, u[h]))) {
-          const bool e1 = lb < n && thi[c1[h] * n + lb] == (uint32_t)(u[h] >> 32) &&
-                          C.tables[(long long)c1[h] * n + lb] == u[h];
-          v1[h] = lb - (e1 ? 1 : 0);  // table c1 has the same lower bound
-        } else {
-          full1 |= 1u << h;
-        }
-      }
-      if (__ballot(full1 != 0)) {  // rare: a full search of table c1
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          lo[h] = 0;
-          len[h] = (full1 >> h) & 1 ? n : 0;
-        }
-        for (;;) {
-          bool more = false;
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-            if (len[h] > 0) {
-              const int half = len[h] >> 1;
-              if (!ge(c1[h], lo[h] + half, u[h])) {
-                lo[h] += half + 1;
-                len[h] -= half + 1;
-              } else {
-                len[h] = half;
-              }
-              more |= len[h] > 0;
-            }
-          if (!__ballot(more)) break;
-        }
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-          if ((full1 >> h) & 1) {
-            const int lb = lo[h];
-            const bool e1 = lb < n && C.tables[(long long)c1[h] * n + lb] == u[h];
-            v1[h] = lb - (e1 ? 1 : 0);
-          }
+        v0[h] = lo + cnt;
+        if (len > 3 || tie || v0[h] > jmax[c0[h]]) slow |= 1u << h;
       }
       int64_t res[4];
+      uint32_t pend = 0;
 #pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        res[h] = (int64_t)v1[h] + C.tail_lo + (int64_t)flo[h];
-        if (v0[h] != v1[h]) {  // the tail: p < cdf -> v0's value (twin_cdt.go:95-110)
-          const double p = __ull2double_rn(u[h]) / 18446744073709551616.0;
-          const double lo_b = a.cdt_sbound[(c0[h] + 1) * sstride + v0[h] + 1] * (1.0 - 9.094947017729282e-13);
-          const double hi_b = a.cdt_sbound[c0[h] * sstride + v0[h] + 1] * (1.0 + 9.094947017729282e-13);
-          if (p < lo_b)
-            res[h] = (int64_t)v0[h] + C.tail_lo + (int64_t)flo[h];
-          else if (!(p >= hi_b))
-            pend |= 1u << h;  // within the bounds' band: sum the terms below
-        }
+      for (int h = 0; h < 4; ++h) res[h] = (int64_t)v0[h] + C.tail_lo + (int64_t)flo[h];
+      if (__ballot(slow != 0)) {  // the exact path, literally (rare)
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if ((slow >> h) & 1) {
+            const int a0 = c0[h], a1 = (int)((int64_t)ceil(128.0 * cf[h]) % 128);
+            const int w0 = cdt_search_hi(thi + a0 * n, C.tables + (long long)a0 * n, n, u[h]);
+            const int w1 = a1 == a0 ? w0 : cdt_search_hi(thi + a1 * n, C.tables + (long long)a1 * n, n, u[h]);
+            v0[h] = w0;
+            res[h] = (int64_t)w1 + C.tail_lo + (int64_t)flo[h];
+            if (w0 != w1) {  // the tail: p < cdf -> v0's value (twin_cdt.go:95-110)
+              const double p = __ull2double_rn(u[h]) / 18446744073709551616.0;
+              const double lo_b = a.cdt_sbound[(a0 + 1) * sstride + w0 + 1] * (1.0 - 9.094947017729282e-13);
+              const double hi_b = a.cdt_sbound[a0 * sstride + w0 + 1] * (1.0 + 9.094947017729282e-13);
+              if (p < lo_b)
+                res[h] = (int64_t)w0 + C.tail_lo + (int64_t)flo[h];
+              else if (!(p >= hi_b))
+                pend |= 1u << h;  // within the bounds' band: sum the terms below
+            }
+          }
       }
 #if RG_VAR & 1
       pend = 0;
@@ -2114,489 +2075,140 @@ __global__ __launch_bounds__(256) void cdt_tail_kernel(SampleArgs a) {
 // Sample() word, from the sampler's own instance (base) or the rounded sampler's (rnd):
 enum { kCoStart = 0, kCoNorm, kCoTailU, kCoTailV, kCoWedge, kCoBit, kCoRR };
 __device__ __forceinline__ int co_src(int st) { return (st >= kCoNorm && st <= kCoWedge) ? 1 : 0; }
-
-struct CosacLane {
-  long long g;     // queue index of the current sample, -1: none
-  long long* out;  // its output word
-  unsigned long long inst;
-  int st, zi;
-  uint64_t pos[2], spare[2];
-  bool have[2];
-  uint64_t zb;
-  double sd, two_s2, lead, inv_lead, c_int, c_frac, x, u, y, y_round;
-};
-
 __device__ __forceinline__ double float52(uint64_t w) { return (double)(w & 0xFFFFFFFFFFFFFull) * 2.220446049250313e-16; }
 
-__device__ __forceinline__ void cosac_step(CosacLane& L, uint64_t w, const ZigDev& Z) {
-  const double rn = 3.442619855899;
-  const int st = L.st;
-  const double fw = float52(w);
-  // the one exp / log a state may need, evaluated once for all lanes that need it.  The exp is
-  // skipped where its comparison is decided without it: START rejects when r >= 1 / lead
-  // (exp <= 1, and / is monotone); RR accepts when arg >= 0 (exp >= 1 > rr) or when
-  // rr < (1 + arg)(1 - 2^-48) <= exp(arg) (exp(a) >= 1 + a; exp within an ulp)
-  double arg = 0.0;
-  bool need_e = false, acc = false;
-  if (st == kCoStart) {
-    arg = -(L.c_frac * L.c_frac) / L.two_s2;
-    need_e = fw < L.inv_lead;
-  }
-  if (st == kCoWedge) {
-    arg = -0.5 * L.x * L.x;
-    need_e = true;
-  }
-  if (st == kCoRR) {
-    arg = -((L.y_round + L.c_frac) * (L.y_round + L.c_frac) - L.y * L.y) / L.two_s2;
-    acc = arg >= 0.0 || fw < (1.0 + arg) * 0.99999999999999644729;
-    need_e = !acc;
-  }
-  double e = 0.0, lg = 0.0;
-  if (need_e) e = exp(arg);
-  if (st == kCoTailU || st == kCoTailV) lg = -log(fw);
-  double nf = 0.0;
-  bool have_nf = false;
-  switch (st) {
-    case kCoStart:  // gaussian_cosac.go:36-40
-      if (need_e && fw < e / L.lead) {
-        *L.out = (int64_t)L.c_int;
-        L.g = -1;
-      } else {
-        L.st = kCoNorm;
-      }
-      break;
-    case kCoNorm: {  // gaussian_rounded.go:80-92
-      const uint64_t b = w >> 63;
-      const uint32_t i = (uint32_t)(w & 127u);
-      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
-      const double x = (double)(int64_t)((j ^ (0ull - b)) + b) * Z.wn[i];
-      if (j < Z.kn[i]) {
-        nf = x;
-        have_nf = true;
-      } else if (i == 0) {
-        L.zb = b;
-        L.st = kCoTailU;
-      } else {
-        L.zi = (int)i;
-        L.x = x;
-        L.st = kCoWedge;
-      }
-      break;
-    }
-    case kCoTailU:  // gaussian_rounded.go:94-101
-      L.u = lg * (1.0 / rn);
-      L.st = kCoTailV;
-      break;
-    case kCoTailV:
-      if (lg + lg >= L.u * L.u) {
-        const double uu = L.u + rn;
-        nf = L.zb == 1 ? -uu : uu;
-        have_nf = true;
-      } else {
-        L.st = kCoTailU;
-      }
-      break;
-    case kCoWedge: {  // gaussian_rounded.go:109-113
-      const double f0 = Z.fn[L.zi - 1], f1 = Z.fn[L.zi];
-      if (fw * (f0 - f1) < e - f1) {
-        nf = L.x;
-        have_nf = true;
-      } else {
-        L.st = kCoNorm;
-      }
-      break;
-    }
-    case kCoBit: {  // gaussian_cosac.go:43-50
-      bool cmp;
-      if ((w & 1) == 0) {
-        L.y_round = round(L.y) - 1.0;
-        cmp = L.y_round <= 0.5;
-      } else {
-        L.y_round = round(L.y) + 1.0;
-        cmp = L.y_round >= -0.5;
-      }
-      L.st = cmp ? kCoRR : kCoNorm;
-      break;
-    }
-    default:  // kCoRR, gaussian_cosac.go:51-55
-      if (acc || fw < e) {
-        *L.out = (int64_t)L.y_round + (int64_t)L.c_int;
-        L.g = -1;
-      } else {
-        L.st = kCoNorm;
-      }
-      break;
-  }
-  if (have_nf) {
-    L.y = L.sd * nf;
-    L.st = kCoBit;
-  }
-}
-
-// COSAC with its words precomputed: KB blocks (2 KB words) of the sampler's own instance and
-// KR blocks of the rounded sampler's, all lanes in lockstep, then the reference's control flow
-// (gaussian_cosac.go:22-57, normFloat's fast path gaussian_rounded.go:80-92) from registers
-// for up to 2 KR rejection-loop passes.  Returns false (nothing written) when the sample needs
-// more: a ziggurat wedge/tail draw, more passes or more words; the caller restarts it with
-// more blocks or in the state machine.  Exp shortcuts as in cosac_step.
-template <int KB, int KR>
-__device__ __forceinline__ bool cosac_fast(const LdsKey& kb, const LdsKey& kr, const uint32_t* lds,
-                                           unsigned long long inst, double center, double sd, const ZigDev& Z,
-                                           long long& res) {
-  uint64_t bw[2 * KB], rw[2 * KR];
-#pragma unroll
-  for (int i = 0; i < KB; ++i) ks_words(kb, inst, (uint64_t)i, lds, bw[2 * i], bw[2 * i + 1]);
-#pragma unroll
-  for (int i = 0; i < KR; ++i) ks_words(kr, inst, (uint64_t)i, lds, rw[2 * i], rw[2 * i + 1]);
-  const double two_s2 = 2.0 * sd * sd;
-  const double lead = sqrt(2.0 * M_PI) * sd;
-  const double c_int = round(center);
-  const double c_frac = c_int - center;
-  const double r = float52(bw[0]);
-  if (r < 1.0 / lead && r < exp(-(c_frac * c_frac) / two_s2) / lead) {
-    res = (long long)c_int;
-    return true;
-  }
-  int bp = 1;
-  bool done = false, fail = false;
-#pragma unroll
-  for (int it = 0; it < 2 * KR; ++it) {
-    if (!done && !fail) {
-      const uint64_t w = rw[it];
-      const uint64_t sb = w >> 63;
-      const uint32_t i = (uint32_t)(w & 127u);
-      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
-      if (!(j < Z.kn[i])) {
-        fail = true;  // normFloat's wedge / tail: more rounded-sampler words
-      } else {
-        const double y = sd * ((double)(int64_t)((j ^ (0ull - sb)) + sb) * Z.wn[i]);
-        uint64_t wb = 0;
-#pragma unroll
-        for (int q = 1; q < 2 * KB; ++q)
-          if (q == bp) wb = bw[q];
-        if (bp >= 2 * KB) fail = true;
-        ++bp;
-        double y_round;
-        bool cmp;
-        if ((wb & 1) == 0) {
-          y_round = round(y) - 1.0;
-          cmp = y_round <= 0.5;
-        } else {
-          y_round = round(y) + 1.0;
-          cmp = y_round >= -0.5;
-        }
-        if (!fail && cmp) {
-          uint64_t wr = 0;
-#pragma unroll
-          for (int q = 1; q < 2 * KB; ++q)
-            if (q == bp) wr = bw[q];
-          if (bp >= 2 * KB) fail = true;
-          ++bp;
-          if (!fail) {
-            const double rr = float52(wr);
-            const double arg = -((y_round + c_frac) * (y_round + c_frac) - y * y) / two_s2;
-            if (arg >= 0.0 || rr < (1.0 + arg) * 0.99999999999999644729 || rr < exp(arg)) {
-              res = (long long)y_round + (long long)c_int;
-              done = true;
-            }
-          }
-        }
-      }
-    }
-  }
-  return done;
-}
-
-// COSAC polynomials: row 0 of the data columns (ecdBlindStdDev) and the mask column
-// (maskBlindStdDev, maskStdDev); job j of a commit is (j, 0) for j < cols, else
-// (cols, j - cols).  Each wave owns jobs wid, wid + nwaves, ... and works in three phases:
-//   1. every sample: cosac_fast<2, 1> (3 blocks; resolves ~3/4: <= 2 loop passes);
-//   2. the rest, restarted: cosac_fast<3, 2> (5 blocks; <= 4 passes);
-//   3. the rest (~1/16), restarted in the state machine below: a queue that lanes refill as
-//      they accept; per iteration every lane first consumes its buffered words, then ONE AES
-//      block is computed for all lanes that need a new one.
-// Unresolved samples go to the wave's segment of a.cos_seg as enc_noise index | sd code << 62
-// (phase 2 compacts it in place).  The deltaInv centres were written into enc_noise by
-// cdt_noise_kernel; instance = polys_before * 256 + enc_noise index.
-constexpr int kCosacThreads = 512;
-__global__ __launch_bounds__(kCosacThreads) void cosac_noise_kernel(SampleArgs a) {
-  __shared__ uint32_t lds[kAesLds];
-  __shared__ uint32_t keys[2][kKeyWords];
-  __shared__ uint64_t zig[384];  // kn, wn, fn
-  aes_lds_fill(lds, a.te0);
-  aes_key_fill(keys[0], a.key[kDomCosac]);
-  aes_key_fill(keys[1], a.key[kDomCosacRnd]);
-  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
-    zig[i] = a.zig.kn[i];
-    zig[128 + i] = __double_as_longlong(a.zig.wn[i]);
-    zig[256 + i] = __double_as_longlong(a.zig.fn[i]);
-  }
-  __syncthreads();
-  const ZigDev Z{zig, reinterpret_cast<const double*>(zig + 128), reinterpret_cast<const double*>(zig + 256)};
-  const LdsKey kb{keys[0]}, kr{keys[1]};
-  const JShape& S = a.s;
-  const int lane = threadIdx.x & 63;
-  const long long nwaves = (long long)gridDim.x * (kCosacThreads / 64);
-  const long long wid = (long long)blockIdx.x * (kCosacThreads / 64) + (threadIdx.x >> 6);
-  const int per = S.cols + S.rows;
-  const long long njobs = a.batch * per;
-  const unsigned long long pb256 = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * 256ull;
-  const double sds[3] = {a.sd_ecd_blind, a.sd_mask, a.sd_mask_blind};
-  unsigned long long* seg = a.cos_seg + wid * a.cos_cap;
-  auto mb = [](uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-  };
-  // ---- phase 1 ----
-  long long nseg = 0;
-  for (long long job = wid; job < njobs; job += nwaves) {
-    const long long b = job / per;
-    const int j = (int)(job % per);
-    const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
-    const int code = col < S.cols ? 0 : (row == 0 ? 2 : 1);
-    const double sd = sds[code];
-    if (enc_skipped(S, col, row) || sd == a.sd_ecd) continue;
-    const long long poly = (b * (S.cols + 1) + col) * S.rows + row;
-    for (int k = lane; k < 256; k += 64) {
-      const unsigned long long oi = (unsigned long long)(poly * 256 + k);
-      long long res = 0;
-      const bool ok = cosac_fast<2, 1>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sd, Z, res);
-      if (ok) a.enc_noise[oi] = res;
-      const uint64_t fm = __ballot(!ok);
-      if (!ok) seg[nseg + mb(fm)] = oi | ((unsigned long long)code << 62);
-      nseg += __builtin_popcountll(fm);
-    }
-  }
-  // ---- phase 2 (in-place compaction: entry i is read before any write at index <= i) ----
-  long long n2 = 0;
-  for (long long i0 = 0; i0 < nseg; i0 += 64) {
-    const bool act = i0 + lane < nseg;
-    const unsigned long long ent = act ? seg[i0 + lane] : 0;
-    const unsigned long long oi = ent & ((1ull << 62) - 1);
-    bool ok = true;
-    if (act) {
-      long long res = 0;
-      ok = cosac_fast<3, 2>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sds[ent >> 62], Z, res);
-      if (ok) a.enc_noise[oi] = res;
-    }
-    const uint64_t fm = __ballot(!ok);
-    if (!ok) seg[n2 + mb(fm)] = ent;
-    n2 += __builtin_popcountll(fm);
-  }
-  // ---- phase 2b: the rest again with 7 blocks (<= 6 loop passes), so that the state machine
-  // below, which pays a whole-wave AES block per consumed word, sees ~1/4 of phase 2's rest ----
-  {
-    long long n3 = 0;
-    for (long long i0 = 0; i0 < n2; i0 += 64) {
-      const bool act = i0 + lane < n2;
-      const unsigned long long ent = act ? seg[i0 + lane] : 0;
-      const unsigned long long oi = ent & ((1ull << 62) - 1);
-      bool ok = true;
-      if (act) {
-        long long res = 0;
-        ok = cosac_fast<4, 3>(kb, kr, lds, pb256 + oi, __longlong_as_double(a.enc_noise[oi]), sds[ent >> 62], Z, res);
-        if (ok) a.enc_noise[oi] = res;
-      }
-      const uint64_t fm = __ballot(!ok);
-      if (!ok) seg[n3 + mb(fm)] = ent;
-      n3 += __builtin_popcountll(fm);
-    }
-    n2 = n3;
-  }
-  // ---- phase 3: the state machine over the n2 remaining samples ----
-  CosacLane L;
-  L.g = -1;
-  L.st = 0;
-  long long next = 0;
-  for (;;) {
-    const uint64_t need = __ballot(L.g < 0);
-    const int rank = mb(need);
-    if (L.g < 0 && next + rank < n2) {  // take the next sample of the queue
-      L.g = next + rank;
-      const unsigned long long ent = seg[L.g];
-      const unsigned long long oi = ent & ((1ull << 62) - 1);
-      L.sd = sds[ent >> 62];
-      L.out = a.enc_noise + oi;
-      const double center = __longlong_as_double(*L.out);
-      L.inst = pb256 + oi;
-      L.two_s2 = 2.0 * L.sd * L.sd;
-      L.lead = sqrt(2.0 * M_PI) * L.sd;
-      L.inv_lead = 1.0 / L.lead;
-      L.c_int = round(center);
-      L.c_frac = L.c_int - center;
-      L.st = kCoStart;
-      L.pos[0] = L.pos[1] = 0;
-      L.have[0] = L.have[1] = false;
-    }
-    next += __builtin_popcountll(need);
-    if (!__ballot(L.g >= 0)) break;
-    // 1. buffered words (the second word of the instance's last block)
-    for (;;) {
-      const int s = co_src(L.st);
-      const bool can = L.g >= 0 && L.have[s];
-      if (!__ballot(can)) break;
-      if (can) {
-        L.have[s] = false;
-        ++L.pos[s];
-        cosac_step(L, L.spare[s], Z);
-      }
-    }
-    // 2. one keystream block for every lane whose next word starts a new block
-    if (L.g >= 0) {
-      const int s = co_src(L.st);
-      const uint64_t p = L.pos[s];
-      uint64_t w0, w1;
-      if (p < 1024) {
-        ks_words(LdsKey{keys[s]}, L.inst, p / 2, lds, w0, w1);
-        L.spare[s] = w1;
-        L.have[s] = true;
-      } else {  // past the first 8 KiB buffer: the XOR-accumulated refill (rare)
-        w0 = uniform_word_at(LdsKey{keys[s]}, lds, L.inst, p);
-      }
-      ++L.pos[s];
-      cosac_step(L, w0, Z);
-    }
-  }
-}
-#pragma clang fp contract(on)
-
-// ---- cosac2: every COSAC sample through one state machine, one AES block per lane per step ----
-// cosac_noise_kernel precomputes 3 / 5 / 7 keystream blocks per sample in lockstep phases and
-// recomputes them from scratch for the samples a phase leaves open (~5 blocks per sample against
-// the ~3.7 that per-sample instances need), with 236 VGPRs (2 waves per SIMD: the AES lookups'
-// LDS latency is exposed).  Here each wave's samples (its jobs' 256 coefficients each, in order)
-// form a queue; a lane takes the next sample when its current one is done, and every iteration
+// ---- cosac2: COSAC samples through one state machine, one AES block per lane per step ------
+// The COSAC samples of an encode polynomial come in groups of kCosGroup consecutive
+// coefficients; group g of polynomial gpoly draws from instance gpoly * (d / kCosGroup) + g of
+// both COSAC domains (the sampler's own UniformSampler and its RoundedGaussianSampler's), in
+// coefficient order, each sample continuing the streams where the previous one stopped (as one
+// Go COSACSampler would over those samples).  Per-sample instances (round 2) left the unused
+// second word of each instance's last block behind: ~3.7 blocks per sample against ~3.0 here.
+// Each wave's groups (its jobs' 16 groups each, in order) form a queue; a lane takes the next
+// group when its current one is done, and every iteration
 //   1. lets each lane consume its buffered word (the second word of its stream's last block)
 //      while the state machine wants a word it has, then
-//   2. computes ONE AES block per lane: the next block of whichever stream (the sampler's own
-//      instance or its rounded sampler's) the lane's state needs, keys selected per lane from LDS,
-//      and consumes its first word.
-// So every lane with work computes a useful block on every iteration; the words drawn are those
-// of cosac_noise_kernel (same instances, same order), so the outputs are identical.  The lane
-// state is kept small (x / u / y share a register: each is live in disjoint states).
+//   2. computes ONE AES block per lane: the next block of whichever stream the lane's state
+//      needs (keys selected per lane from LDS), and steps on its first word,
+// so every lane with work computes a useful block on every iteration (a block is only ever
+// computed when its first word is consumed at once).  The lane state is kept small (x / u / y
+// share a register: each is live in disjoint states).
 constexpr int kCos2Threads = 1024;
 constexpr int kCos2KeyStride = kKeyWords + 4;  // keys of the two streams 4 banks apart
 
 struct Cos2Lane {
-  int g;                // queue index of the current sample, -1: none
-  int st;               // state | zi << 8 | zb << 15 | code << 16
-  unsigned long long oi;  // enc_noise index
+  int g;                // queue index of the current group, -1: none
+  int st;               // state | zi << 8 | zb << 15 | code << 16 | sample-in-group << 20
+  unsigned long long oi;  // enc_noise index of the current sample
   uint32_t pos[2];      // next word of each stream's instance
   uint32_t have;        // bit s: spare[s] holds word pos[s]
   uint64_t spare[2];
   double c_int, c_frac, t, y_round;  // t: x (wedge), u (tail), y (bit / rr)
 };
 
+// One step of the state machine on word w; returns true when the sample is done (its output
+// written).  Only the common states (Norm, Bit, RR without its exp) run unconditionally; the
+// divisions and exp / log of the reference's comparisons sit in branches that only lanes
+// needing them take:
+//   START  r < exp(-(cFrac^2) / 2 sd^2) / (sqrt(2 pi) sd) can only hold when r < 1 / (sqrt(2 pi) sd)
+//          (exp <= 1): the exp and division only then;
+//   RR     rr < exp(arg), arg = -((yR + cFrac)^2 - y^2) / 2 sd^2 = -D / 2 sd^2: accepted when D <= 0
+//          (arg >= +-0, exp >= 1 > rr), or when rr < (1 + a')(1 - 2^-48) with a' = -D (1 / 2 sd^2)
+//          (1 + 2^-50) <= arg (the product form of the quotient, its rounding covered by the
+//          2^-50) and exp(arg) >= 1 + arg (exp within an ulp, covered by the 2^-48); else the
+//          reference's division and exp decide.
 template <class Z>
-__device__ __forceinline__ void cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, const double* sdv, long long* en) {
+__device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, const double* sdv, long long* en) {
   const double rn = 3.442619855899;
-  const int st = L.st & 255, code = L.st >> 16;
-  const double sd = sdv[4 * code], two_s2 = sdv[4 * code + 1], lead = sdv[4 * code + 2], inv_lead = sdv[4 * code + 3];
+  const int st = L.st & 255, code = (L.st >> 16) & 3;
   const double fw = float52(w);
-  double arg = 0.0;
-  bool need_e = false, acc = false;
-  if (st == kCoStart) {
-    arg = -(L.c_frac * L.c_frac) / two_s2;
-    need_e = fw < inv_lead;
-  }
-  if (st == kCoWedge) {
-    arg = -0.5 * L.t * L.t;
-    need_e = true;
-  }
-  if (st == kCoRR) {
-    arg = -((L.y_round + L.c_frac) * (L.y_round + L.c_frac) - L.t * L.t) / two_s2;
-    acc = arg >= 0.0 || fw < (1.0 + arg) * 0.99999999999999644729;
-    need_e = !acc;
-  }
-  double e = 0.0, lg = 0.0;
-  if (need_e) e = exp(arg);
-  if (st == kCoTailU || st == kCoTailV) lg = -log(fw);
+  bool have_nf = false, done = false;
   double nf = 0.0;
-  bool have_nf = false;
   int nst = st;
-  switch (st) {
-    case kCoStart:  // gaussian_cosac.go:36-40
-      if (need_e && fw < e / lead) {
-        en[L.oi] = (long long)L.c_int;
-        L.g = -1;
-      } else {
-        nst = kCoNorm;
-      }
-      break;
-    case kCoNorm: {  // gaussian_rounded.go:80-92
-      const uint64_t b = w >> 63;
-      const uint32_t i = (uint32_t)(w & 127u);
-      const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
-      const double x = (double)(int64_t)((j ^ (0ull - b)) + b) * Zg.wn[i];
-      if (j < Zg.kn[i]) {
-        nf = x;
-        have_nf = true;
-      } else if (i == 0) {
-        L.st = (L.st & ~(1 << 15)) | ((int)b << 15);
-        nst = kCoTailU;
-      } else {
-        L.st = (L.st & ~(127 << 8)) | ((int)i << 8);
-        L.t = x;
-        nst = kCoWedge;
-      }
-      break;
+  if (st == kCoNorm) {  // gaussian_rounded.go:80-92
+    const uint64_t b = w >> 63;
+    const uint32_t i = (uint32_t)(w & 127u);
+    const uint64_t j = (w >> 7) & 0xFFFFFFFFFFFFFull;
+    const double x = (double)(int64_t)((j ^ (0ull - b)) + b) * Zg.wn[i];
+    if (j < Zg.kn[i]) {
+      nf = x;
+      have_nf = true;
+    } else if (i == 0) {
+      L.st = (L.st & ~(1 << 15)) | ((int)b << 15);
+      nst = kCoTailU;
+    } else {
+      L.st = (L.st & ~(127 << 8)) | ((int)i << 8);
+      L.t = x;
+      nst = kCoWedge;
     }
-    case kCoTailU:  // gaussian_rounded.go:94-101
+  } else if (st == kCoBit) {  // gaussian_cosac.go:43-50
+    bool cmp;
+    if ((w & 1) == 0) {
+      L.y_round = round(L.t) - 1.0;
+      cmp = L.y_round <= 0.5;
+    } else {
+      L.y_round = round(L.t) + 1.0;
+      cmp = L.y_round >= -0.5;
+    }
+    nst = cmp ? kCoRR : kCoNorm;
+  } else if (st == kCoRR) {  // gaussian_cosac.go:51-55
+    const double D = (L.y_round + L.c_frac) * (L.y_round + L.c_frac) - L.t * L.t;
+    bool acc = D <= 0.0;
+    if (!acc) {
+      const double ap = -D * sdv[4 * code + 1] * (1.0 + 8.881784197001252e-16);  // a' <= arg < 0
+      acc = fw < (1.0 + ap) * 0.99999999999999644729;
+      if (!acc) acc = fw < exp(-D / (2.0 * sdv[4 * code] * sdv[4 * code]));
+    }
+    if (acc) {
+      en[L.oi] = (long long)L.y_round + (long long)L.c_int;
+      done = true;
+    } else {
+      nst = kCoNorm;
+    }
+  } else if (st == kCoStart) {  // gaussian_cosac.go:36-40
+    nst = kCoNorm;
+    if (fw < sdv[4 * code + 3]) {  // r < 1 / lead: the reference's exp comparison decides
+      const double sd = sdv[4 * code];
+      if (fw < exp(-(L.c_frac * L.c_frac) / (2.0 * sd * sd)) / sdv[4 * code + 2]) {
+        en[L.oi] = (long long)L.c_int;
+        done = true;
+      }
+    }
+  } else if (st == kCoWedge) {  // gaussian_rounded.go:109-113
+    const int zi = (L.st >> 8) & 127;
+    const double f0 = Zg.fn[zi - 1], f1 = Zg.fn[zi];
+    if (fw * (f0 - f1) < exp(-0.5 * L.t * L.t) - f1) {
+      nf = L.t;
+      have_nf = true;
+    } else {
+      nst = kCoNorm;
+    }
+  } else {  // kCoTailU / kCoTailV, gaussian_rounded.go:94-101
+    const double lg = -log(fw);
+    if (st == kCoTailU) {
       L.t = lg * (1.0 / rn);
       nst = kCoTailV;
-      break;
-    case kCoTailV:
-      if (lg + lg >= L.t * L.t) {
-        const double uu = L.t + rn;
-        nf = ((L.st >> 15) & 1) ? -uu : uu;
-        have_nf = true;
-      } else {
-        nst = kCoTailU;
-      }
-      break;
-    case kCoWedge: {  // gaussian_rounded.go:109-113
-      const int zi = (L.st >> 8) & 127;
-      const double f0 = Zg.fn[zi - 1], f1 = Zg.fn[zi];
-      if (fw * (f0 - f1) < e - f1) {
-        nf = L.t;
-        have_nf = true;
-      } else {
-        nst = kCoNorm;
-      }
-      break;
+    } else if (lg + lg >= L.t * L.t) {
+      const double uu = L.t + rn;
+      nf = ((L.st >> 15) & 1) ? -uu : uu;
+      have_nf = true;
+    } else {
+      nst = kCoTailU;
     }
-    case kCoBit: {  // gaussian_cosac.go:43-50
-      bool cmp;
-      if ((w & 1) == 0) {
-        L.y_round = round(L.t) - 1.0;
-        cmp = L.y_round <= 0.5;
-      } else {
-        L.y_round = round(L.t) + 1.0;
-        cmp = L.y_round >= -0.5;
-      }
-      nst = cmp ? kCoRR : kCoNorm;
-      break;
-    }
-    default:  // kCoRR, gaussian_cosac.go:51-55
-      if (acc || fw < e) {
-        en[L.oi] = (long long)L.y_round + (long long)L.c_int;
-        L.g = -1;
-      } else {
-        nst = kCoNorm;
-      }
-      break;
   }
   if (have_nf) {
-    L.t = sd * nf;
+    L.t = sdv[4 * code] * nf;
     nst = kCoBit;
   }
   L.st = (L.st & ~255) | nst;
+  return done;
 }
 
 __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
   __shared__ uint32_t keys[2 * kCos2KeyStride];
   __shared__ uint64_t zig[384];  // kn, wn, fn
-  __shared__ double sdv[12];     // per sd code: sd, 2 sd^2, sqrt(2 pi) sd, 1 / that
+  __shared__ double sdv[12];     // per sd code: sd, 1 / (2 sd^2), sqrt(2 pi) sd, 1 / that
   aes_lds_fill(lds, a.te0);
   aes_key_fill(keys, a.key[kDomCosac]);
   aes_key_fill(keys + kCos2KeyStride, a.key[kDomCosacRnd]);
@@ -2609,7 +2221,7 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
     const double sd = threadIdx.x == 0 ? a.sd_ecd_blind : threadIdx.x == 1 ? a.sd_mask : a.sd_mask_blind;
     const double lead = sqrt(2.0 * M_PI) * sd;
     sdv[4 * threadIdx.x] = sd;
-    sdv[4 * threadIdx.x + 1] = 2.0 * sd * sd;
+    sdv[4 * threadIdx.x + 1] = 1.0 / (2.0 * sd * sd);
     sdv[4 * threadIdx.x + 2] = lead;
     sdv[4 * threadIdx.x + 3] = 1.0 / lead;
   }
@@ -2622,42 +2234,50 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
   const int per = S.cols + S.rows;
   const long long njobs = a.batch * per;
   const long long myjobs = njobs > wid ? (njobs - wid + nwaves - 1) / nwaves : 0;
-  const long long total = myjobs * 256;  // this wave's queue
-  const unsigned long long pb256 = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * 256ull;
+  constexpr int NG = 256 / kCosGroup;  // groups per polynomial
+  const long long total = myjobs * NG;  // this wave's queue of groups
+  const unsigned long long pbg = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * (unsigned long long)NG;
   auto mb = [](uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  };
+  auto start_sample = [&](Cos2Lane& L) {  // the group's next sample: its centre, state START
+    const double center = __longlong_as_double(a.enc_noise[L.oi]);
+    L.c_int = round(center);
+    L.c_frac = L.c_int - center;
+    L.st = (L.st & ~0xFFFF) | kCoStart;
   };
   Cos2Lane L;
   L.g = -1;
   L.st = 0;
+  unsigned long long inst = 0;  // the group's instance (both streams)
   long long next = 0;
   for (;;) {
     bool can = L.g >= 0 && ((L.have >> co_src(L.st & 255)) & 1);
     uint64_t w = 0;
     if (!__ballot(can)) {
-      // no lane can step on a buffered word: lanes without a sample take the next ones of the
-      // queue (samples of jobs that draw nothing are dropped here), then every lane with work
-      // computes the next block of the stream its state needs and steps on its first word
+      // no lane can step on a buffered word: lanes without a group take the next ones of the
+      // queue (groups of polynomials that draw nothing are dropped here), then every lane with
+      // work computes the next block of the stream its state needs and steps on its first word
       for (;;) {
         const uint64_t need = __ballot(L.g < 0);
         if (!need || next >= total) break;
         const int rank = mb(need);
         if (L.g < 0 && next + rank < total) {
           const long long g = next + rank;
-          const long long job = wid + (g >> 8) * nwaves;
+          const long long job = wid + (g / NG) * nwaves;
           const long long b = job / per;
           const int j = (int)(job % per);
           const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
           const int code = col < S.cols ? 0 : (row == 0 ? 2 : 1);
           if (!enc_skipped(S, col, row) && sdv[4 * code] != a.sd_ecd) {
+            const long long poly = (b * (S.cols + 1) + col) * S.rows + row;
             L.g = (int)g;
-            L.oi = (unsigned long long)(((b * (S.cols + 1) + col) * S.rows + row) * 256 + (g & 255));
-            const double center = __longlong_as_double(a.enc_noise[L.oi]);
-            L.c_int = round(center);
-            L.c_frac = L.c_int - center;
-            L.st = kCoStart | (code << 16);
+            L.oi = (unsigned long long)(poly * 256 + (g % NG) * kCosGroup);
+            inst = pbg + (unsigned long long)(poly * NG + g % NG);
+            L.st = code << 16;
             L.pos[0] = L.pos[1] = 0;
             L.have = 0;
+            start_sample(L);
           }
         }
         next += __builtin_popcountll(need);
@@ -2667,7 +2287,6 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
         const int s = co_src(L.st & 255);
         const uint32_t p = L.pos[s];
         const LdsKey k{keys + s * kCos2KeyStride};
-        const unsigned long long inst = pb256 + L.oi;
         if (p < 1024) {
           uint64_t w1;
           ks_words(k, inst, p / 2, lds, w, w1);
@@ -2689,10 +2308,21 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
     }
     if (can) {
       ++L.pos[co_src(L.st & 255)];
-      cos2_step(L, w, Z, sdv, a.enc_noise);
+      if (cos2_step(L, w, Z, sdv, a.enc_noise)) {  // done: the group's next sample continues its streams
+        const int kk = ((L.st >> 20) & 15) + 1;
+        if (kk == kCosGroup) {
+          L.g = -1;
+        } else {
+          L.st = (L.st & ~(15 << 20)) | (kk << 20);
+          ++L.oi;
+          start_sample(L);
+        }
+      }
     }
   }
 }
+
+#pragma clang fp contract(on)
 
 // thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
 __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
@@ -3033,7 +2663,6 @@ struct rg_jindo_scratch {
   rg::DevBuf digits, com, ocom;
   rg::DevBuf last, mask, en, mn;  // the sampled randomness of rg_jindo_commit_sampled_dev
   rg::DevBuf tails, tail_n;       // deferred TwinCDT tails (cdt_noise_kernel -> cdt_tail_kernel)
-  rg::DevBuf cos_seg;             // COSAC samples carried between the phases of cosac_noise_kernel
 };
 
 // Sampler setup (rg_jindo_set_stddevs): the reference's six standard deviations and the tables
@@ -3041,7 +2670,7 @@ struct rg_jindo_scratch {
 struct rg_jindo_samplers {
   bool ready = false;
   double sd[6];  // ecd, ecd_blind, mask, mask_blind, mlwe, mask_mlwe
-  rg::DevBuf te0, cdt_enc, cdt_guide, cdt_sbound, cdt_mlwe, zig, delta;
+  rg::DevBuf te0, cdt_enc, cdt_guide, cdt_sbound, cdt_jmax, cdt_mlwe, zig, delta;
   int cdt_enc_size = 0, cdt_mlwe_size = 0;
   int64_t tail_lo_enc = 0, tail_lo_mlwe = 0;
   std::vector<double> h_delta;
@@ -3636,6 +3265,7 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     a.tails = sc->tails.as<CdtTail>();
     a.tail_n = sc->tail_n.as<int>();
     a.cdt_sbound = S.cdt_sbound.as<double>();
+    a.cdt_jmax = S.cdt_jmax.as<int>();
     static const bool cdt_legacy = [] {  // RINGO_CDT=legacy: cdt_noise_kernel + cdt_tail_kernel (A/B)
       const char* e = getenv("RINGO_CDT");
       return e && e[0] == 'l';
@@ -3653,28 +3283,10 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)nw), dim3(64 * kTailWavesPerSeg), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT tails)"));
     }
-    const long long ncos = (long long)batch * (p.cols + p.rows);  // jobs
-    const long long wpb = kCosacThreads / 64;
-    const unsigned gc = (unsigned)std::min<long long>((ncos + wpb - 1) / wpb, 1024);
-    a.cos_cap = (ncos + (long long)gc * wpb - 1) / ((long long)gc * wpb) * 256;  // every sample of its jobs
-    {
-      std::lock_guard<std::mutex> lk(J->mu);
-      const size_t cb = (size_t)gc * wpb * a.cos_cap * 8;
-      if (sc->cos_seg.bytes < cb) RG_HIP(hipStreamSynchronize(st));
-      RG_TRY(sc->cos_seg.alloc(cb));
-    }
-    a.cos_seg = sc->cos_seg.as<unsigned long long>();
-    static const bool cos_legacy = [] {  // RINGO_COSAC=legacy: the three-phase cosac_noise_kernel (A/B)
-      const char* e = getenv("RINGO_COSAC");
-      return e && e[0] == 'l';
-    }();
-    if (cos_legacy) {
-      hipLaunchKernelGGL(cosac_noise_kernel, dim3(gc), dim3(kCosacThreads), 0, st, a);
-    } else {
-      const long long w2 = kCos2Threads / 64;
-      const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
-      hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
-    }
+    const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
+    const long long w2 = kCos2Threads / 64;
+    const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
+    hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (COSAC)"));
   } else {
     hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 511) / 512)), dim3(512), 0, st, a);
@@ -4361,6 +3973,21 @@ rg_status rg_jindo_set_stddevs(rg_jindo* J, const rg_jindo_stddevs* sd) {
       }
     }
     RG_TRY(S.cdt_sbound.upload(sb.data(), sb.size() * 8));
+    // jmax[c]: the largest J with, for every v0 = j in [-1, J] of table c, the bound on p
+    // (t_c[j + 1] / 2^64, or 1 past the table) below the smallest cdf the reference can compare it
+    // with (S[c + 1][j] (1 - 2^-40)), again shrunk by 2^-40 for the double rounding of p
+    std::vector<int> jm(128);
+    for (int c = 0; c < 128; ++c) {
+      const uint64_t* t = enc.data() + (size_t)c * n;
+      int J = -2;
+      for (int j = -1; j <= n; ++j) {
+        const double pu = (j + 1 < n ? (double)t[j + 1] / 18446744073709551616.0 : 1.0) * (1.0 + 9.094947017729282e-13);
+        if (!(pu < sb[(size_t)(c + 1) * (n + 2) + j + 1] * (1.0 - 9.094947017729282e-13))) break;
+        J = j;
+      }
+      jm[c] = J;
+    }
+    RG_TRY(S.cdt_jmax.upload(jm.data(), jm.size() * 4));
   }
   RG_TRY(S.cdt_mlwe.upload(ml.data(), ml.size() * 8));
   const Ziggurat Z = make_ziggurat();
@@ -4447,7 +4074,11 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   // numbered per commit (first_commit + b0), scratch is per stream, and the aux stream (with its
   // scratch) belongs to this caller stream only, so concurrent callers on different streams never
   // share a buffer.
-  if (batch < 64) return run(0, batch, st);
+  static const bool no_split = [] {  // RINGO_JINDO_SPLIT=0: one stream (per-kernel profiling)
+    const char* e = getenv("RINGO_JINDO_SPLIT");
+    return e && e[0] == '0';
+  }();
+  if (batch < 64 || no_split) return run(0, batch, st);
   hipStream_t aux;
   {
     std::lock_guard<std::mutex> lk(Jm->mu);

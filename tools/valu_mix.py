@@ -18,8 +18,13 @@ COST = {
     # full rate (ops2.hip): plain 32-bit add/sub/logic/moves/shifts, VOP2 cndmask on vcc
     "v_add_u32": FULL, "v_sub_u32": FULL, "v_subrev_u32": FULL, "v_and_b32": FULL, "v_or_b32": FULL,
     "v_xor_b32": FULL, "v_not_b32": FULL, "v_mov_b32": FULL, "v_lshrrev_b32": FULL, "v_ashrrev_i32": FULL,
-    "v_cndmask_b32_e32": FULL, "v_readfirstlane_b32": FULL, "v_readlane_b32": FULL, "v_writelane_b32": FULL,
+    "v_cndmask_b32_e32": FULL, "v_readfirstlane_b32": 4.25, "v_readlane_b32": 4.25, "v_writelane_b32": 4.25,
     "v_mbcnt_lo_u32_b32": FULL, "v_mbcnt_hi_u32_b32": FULL,
+    # ops3.hip (MI355X, round 3): VOP3 / 64-bit / f64 forms and lane ops
+    "v_perm_b32": 4.52, "v_bitop3_b32": 3.67, "v_mov_b64_e32": 4.65, "v_lshl_add_u64": 4.80, "v_lshlrev_b64": 4.18,
+    "v_add_f64": 4.58, "v_mul_f64": 4.25, "v_fma_f64": 4.65, "v_fmac_f64_e32": 4.65, "v_cvt_f32_u32_e32": 4.07,
+    "v_cmp_lt_u64_e32": 4.51, "v_mul_hi_u32_u24_e32": 4.09, "v_mul_u32_u24_e32": 4.26, "v_floor_f64_e32": 4.50,
+    "v_lshl_or_b32": 4.28, "v_exp_f32_e32": 8.15, "v_rcp_f64_e32": 16.41, "v_ldexp_f64": 4.20,
 }
 # half rate (ops2.hip / intmul.hip): multiplies, carry chains, VOP3 three-operand forms, 64-bit ops
 HALF_PREFIX = ("v_mad_u64_u32", "v_mad_i64_i32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_hi_i32", "v_add_co_u32",
