@@ -71,11 +71,13 @@ __device__ __forceinline__ void mont256(uint32_t (&z)[8], const uint32_t (&x)[8]
   z[7] = lo32(A);
 }
 
-// x * 2^-16 mod q for q = 1 mod 2^16 (the N^-1 of N = 2^16, ntt.go:242-243): with
-// k = -x mod 2^16, x + k q is divisible by 2^16 and (x + k q) / 2^16 < 2q for x < 2q.
+// x * 2^-SH mod q for q = 1 mod 2^SH (the N^-1 of N = 2^SH, ntt.go:242-243): with
+// k = -x mod 2^SH, x + k q is divisible by 2^SH and (x + k q) / 2^SH < 2q for x < 2q.
 // q's digits 0, 1 are (1, 0): k q = k + sum_{j>=2} k q_j 2^(32 j).
-__device__ __forceinline__ void div2p16_256(uint32_t (&x)[8], const uint32_t (&q)[8]) {
-  const uint32_t k = (0u - x[0]) & 0xffffu;
+template <int SH>
+__device__ __forceinline__ void div2p_256(uint32_t (&x)[8], const uint32_t (&q)[8]) {
+  static_assert(SH >= 1 && SH <= 31, "shift");
+  const uint32_t k = (0u - x[0]) & ((1u << SH) - 1u);
   uint32_t y[9];
   uint64_t acc = (uint64_t)x[0] + k;
   y[0] = lo32(acc);
@@ -88,7 +90,7 @@ __device__ __forceinline__ void div2p16_256(uint32_t (&x)[8], const uint32_t (&q
   }
   y[8] = hi32(acc);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = __builtin_amdgcn_alignbit(y[j + 1], y[j], 16);
+  for (int j = 0; j < 8; ++j) x[j] = __builtin_amdgcn_alignbit(y[j + 1], y[j], SH);
 }
 
 // x + y (x, y < 2q, sum < 4q < 2^257) -> [0, 2q)
@@ -161,13 +163,18 @@ RG_NTT256_BFLY D16 bfly_inv256(D8 x, D8 y, D8 w, const Ntt256Args* a) {
   return r;
 }
 
-template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL>
+// LOGC: bits of the pass's sub-transform (8: 256 points; 7: the 128-point COL pass of N = 2^15,
+// whose patterns are H x = t + 16 y, M x = (y>>2) 64 + (t>>2) 16 + (y&3) 4 + (t&3), L x = 8 t + r)
+template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, int LOGN = 16, int LOGC = 8>
 __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffer_rsrc_t twr, uint32_t (&e)[8][8],
                                              uint32_t hi, uint32_t t, bool rowuni) {
-  constexpr int G0 = COL ? 0 : 8;
+  constexpr int G0 = COL ? 0 : LOGN - 8;
   auto xof = [&](int rho) -> uint32_t {
-    if (PAT == 0) return t + 32u * rho;
-    if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
+    if (PAT == 0) return t + (1u << (LOGC - 3)) * rho;
+    if (PAT == 1) {
+      if (LOGC == 8) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
+      return ((uint32_t)(rho >> 2) << 6) | ((t >> 2) << 4) | ((uint32_t)(rho & 3) << 2) | (t & 3u);
+    }
     return 8u * t + rho;
   };
   constexpr int NPK = 1 << RK;
@@ -175,7 +182,7 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
   for (int sp = 0; sp < RK; ++sp) {
     const int bw = INV ? sp : (RK - 1 - sp);
     const int b = LO + bw;
-    const int k = 7 - b;
+    const int k = LOGC - 1 - b;
     const int half = 1 << bw;
     const bool last = INV && SCALE && k == 0;
 #pragma unroll
@@ -215,7 +222,7 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
         e[rho1][i] = R.y.d[i];
       }
       if constexpr (INV) {
-        if (last) div2p16_256(e[rho0], a.q);  // (u + v) N^-1, N = 2^16
+        if (last) div2p_256<LOGN>(e[rho0], a.q);  // (u + v) N^-1, N = 2^LOGN
       }
     }
   }
@@ -234,27 +241,34 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
 #ifndef RG_NTT256_WPE
 #define RG_NTT256_WPE 1  // amdgpu_waves_per_eu lower bound (A/B knob)
 #endif
-template <bool INV, bool COL, bool SCALE, bool CANON, bool RP>
+// LOGN = 16 (COL and ROW both 8-stage passes) or 15 (COL: 7 stages on 256 columns of 128 points,
+// 8 of them per tile; ROW: 8 stages on 128 rows of 256 points), as ntt.hip plans them.
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int LOGN = 16>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_WPE))) void ntt256_pass(Ntt256Args a) {
-  constexpr int PITCH = COL ? 296 : 288, PLANE = 4 * PITCH;
+  static_assert(LOGN == 15 || LOGN == 16, "ntt256_pass: N = 2^15 or 2^16");
+  constexpr int LOGC = COL ? LOGN - 8 : 8;        // bits of a sub-transform
+  constexpr uint32_t CPT = COL ? (1024u >> LOGC) : 4u;  // sub-transforms per tile
+  constexpr int PITCH = COL ? (LOGC == 8 ? 296 : 148) : 288, PLANE = (int)CPT * PITCH;
   constexpr int NPL = RG_NTT256_PLANES;  // limb planes per LDS round (4 or 2)
   static_assert(NPL == 4 || NPL == 2, "RG_NTT256_PLANES");
+  constexpr uint32_t R = 1u << (LOGN - 8);  // ROW: rows per polynomial; COL: tiles per polynomial x CPT / 256
   __shared__ uint64_t lds[NPL * PLANE];
   const uint32_t tid = threadIdx.x;
-  const uint32_t s = COL ? (tid & 3u) : (tid >> 5);
-  const uint32_t t = COL ? (tid >> 2) : (tid & 31u);
+  const uint32_t s = COL ? (tid % CPT) : (tid >> 5);
+  const uint32_t t = COL ? (tid / CPT) : (tid & 31u);
   const uint32_t tile = blockIdx.x;
-  // element (32 B) offsets: COL: poly * 2^16 + 4 * column block;  ROW: RP: row (tile & 255) of
-  // polys 4 (tile >> 8) + s, else 4 consecutive rows
-  const size_t tbase = COL  ? (((size_t)(tile >> 6) << 16) + ((tile & 63u) << 2))
-                       : RP ? (((size_t)(tile >> 8) << 18) + ((tile & 255u) << 8))
+  // element (32 B) offsets: COL: poly * 2^LOGN + CPT * column block;  ROW: RP: row (tile % R) of
+  // polys 4 (tile / R) + s, else 4 consecutive rows
+  constexpr uint32_t TPP = 256u / CPT;  // COL tiles per polynomial
+  const size_t tbase = COL  ? (((size_t)(tile / TPP) << LOGN) + (tile % TPP) * CPT)
+                       : RP ? (((size_t)(tile / R) << (LOGN + 2)) + ((tile % R) << 8))
                             : ((size_t)tile << 10);
-  constexpr uint32_t SSH = COL ? 0 : (RP ? 16 : 8);  // log2 sub-transform stride (elements)
-  constexpr uint32_t XSH = COL ? 8 : 0;              // log2 point stride (elements)
+  constexpr uint32_t SSH = COL ? 0 : (RP ? LOGN : 8);  // log2 sub-transform stride (elements)
+  constexpr uint32_t XSH = COL ? 8 : 0;                // log2 point stride (elements)
   const __amdgpu_buffer_rsrc_t rin = rg_buf(a.in + 4 * tbase);
   const __amdgpu_buffer_rsrc_t rout = rg_buf(a.out + 4 * tbase);
   const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
-  const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 2) + s) & 255u);
+  const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile % R) : (((tile << 2) + s) & (R - 1u));
   uint32_t e[8][8];
   auto gload = [&](int reg, uint32_t x) {
     const uint32_t off = ((s << SSH) + (x << XSH)) * 32u;
@@ -271,8 +285,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
     __builtin_amdgcn_raw_buffer_store_b128(v0, rout, off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v1, rout, off + 16u, 0, 0);
   };
-  auto xH = [&](int y) { return t + 32u * y; };
-  auto xM = [&](int y) { return ((t >> 2) << 5) | ((uint32_t)y << 2) | (t & 3u); };
+  auto xH = [&](int y) { return t + (1u << (LOGC - 3)) * y; };
+  auto xM = [&](int y) -> uint32_t {
+    if (LOGC == 8) return ((t >> 2) << 5) | ((uint32_t)y << 2) | (t & 3u);
+    return ((uint32_t)(y >> 2) << 6) | ((t >> 2) << 4) | ((uint32_t)(y & 3) << 2) | (t & 3u);
+  };
   auto xL = [&](int r) { return 8u * t + r; };
   enum { HM, ML, LH };
   auto lpos = [&](uint32_t x, int ph) -> uint32_t {
@@ -311,11 +328,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
   if constexpr (!INV) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) gload(y, xH(y));
-    ntt256_round<3, 5, 0, false, false, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<3, LOGC - 3, 0, false, false, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     xchg(xH, HM, xM, HM, false);
-    ntt256_round<3, 2, 1, false, false, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<LOGC - 5, 2, 1, false, false, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     xchg(xM, ML, xL, ML, true);
-    ntt256_round<2, 0, 2, false, false, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<2, 0, 2, false, false, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     if (CANON) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) canon256(e[r], a.q);
@@ -337,11 +354,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
       for (int y = 0; y < 8; ++y) gload(y, xH(y));
       xchg(xH, LH, xL, LH, false);
     }
-    ntt256_round<2, 0, 2, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<2, 0, 2, true, SCALE, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     xchg(xL, ML, xM, ML, !COL);
-    ntt256_round<3, 2, 1, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<LOGC - 5, 2, 1, true, SCALE, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     xchg(xM, HM, xH, HM, true);
-    ntt256_round<3, 5, 0, true, SCALE, COL>(a, twr, e, hi, t, rowuni);
+    ntt256_round<3, LOGC - 3, 0, true, SCALE, COL, LOGN, LOGC>(a, twr, e, hi, t, rowuni);
     if (CANON) {
 #pragma unroll
       for (int y = 0; y < 8; ++y) canon256(e[y], a.q);

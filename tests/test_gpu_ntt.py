@@ -104,17 +104,19 @@ def test_ntt_2e16_batches_match_oracle(fields, batch):
     assert (x.cpu().numpy().view(np.uint64).reshape(batch, N, 1) == want_inv).all()
 
 
+@pytest.mark.parametrize("logn,negacyclic", [(16, True), (16, False), (15, True), (15, False)])
 @pytest.mark.parametrize("batch", [1, 4, 5])
-def test_ntt_2e16_q255_matches_oracle(fields, batch):
-    """Degree 2^16 at the Jindo default prime (4 limbs, q = 1 mod 2^64): the ntt256 kernels
-    (both ROW tilings: same row of 4 polys when batch % 4 == 0, else 4 rows of one poly),
-    forward vs the C oracle, inverse round trip and inverse of arbitrary input."""
+def test_ntt_2e16_q255_matches_oracle(fields, batch, logn, negacyclic):
+    """Degree 2^16 and 2^15 at the Jindo default prime (4 limbs, q = 1 mod 2^64): the ntt256
+    kernels (N = 2^15: a 7-stage COL pass of 128-point columns, 8 per tile; both ROW tilings: same
+    row of 4 polys when batch % 4 == 0, else 4 rows of one poly), cyclic (Buckler's encoder) and
+    negacyclic, forward vs the C oracle, inverse round trip and inverse of arbitrary input."""
     q = fields["jindo_zp"]
-    N = 1 << 16
+    N = 1 << logn
     F = ringo.Field(q)
     cf = co.CField(q)
-    T = ringo.CyclotomicTransformer(F, N)
-    tw, twi, ninv = cf.tables(N)
+    T = (ringo.CyclotomicTransformer if negacyclic else ringo.CyclicTransformer)(F, N)
+    tw, twi, ninv = cf.tables(N, cyclic=not negacyclic)
     rng = np.random.default_rng(100 + batch)
     a = F.random(batch * N, rng).reshape(batch, N, F.L)
     a[0, 0] = F.mont([q - 1])[0]

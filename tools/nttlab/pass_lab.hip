@@ -249,6 +249,8 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   (void)cus;
   for (int rep = 0; rep < 2; ++rep) {
+    run_chunked<256 + 512>("ntt16 RP", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
+    run_chunked<256 + 512 + 4>("ntt16 RP no-HBM (compute)", base, d_tw, d_twi, d_x, batch, N, 1 << 20);
     run_variant<1, 256>("ntt16 per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
     run_variant<1, 256 + 512>("ntt16 RP per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
     run_variant<1, 256 + 512 + 1>("RP no-tw per-pass", base, d_tw, d_twi, d_x, d_src, d_ref, batch, N, 1 << 30);
