@@ -276,8 +276,10 @@ rg_status rg_jindo_delta_inv(const rg_jindo* j, double* out);
  * MustSetRandom (prover.go:65-139, encoder.go:149-183).  A Go caller draws them from crypto/rand.
  * On the device each sampler instance is a window of its domain's counter space (instance n =
  * the UniformSampler with IV + n 2^24, a 128-bit sum, so the 2^64 instance numbers have disjoint
- * windows): one per encode polynomial (twinCDT), per MLWE polynomial (mlweSampler), per sample
- * (COSAC, rounded) and per field element (uniform), numbered from `first_commit`, the index of
+ * windows): one per encode polynomial (twinCDT), per group of 16 consecutive coefficients of a
+ * COSAC-encoded polynomial (COSAC and its RoundedGaussianSampler, instance poly (d/16) + group),
+ * per MLWE polynomial (mlweSampler), per mask-column MLWE sample (rounded) and per field element
+ * (uniform), numbered from `first_commit`, the index of
  * the batch's first commit among all commits made with these seeds (so batches and GPUs never
  * share keystream).  The sampled entry points return RG_ERR_INVALID when an instance number of
  * commits [first_commit, first_commit + batch) would pass 2^64 - 1, i.e. when

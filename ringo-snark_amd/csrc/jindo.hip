@@ -2228,7 +2228,6 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
   __syncthreads();
   const ZigDev Z{zig, reinterpret_cast<const double*>(zig + 128), reinterpret_cast<const double*>(zig + 256)};
   const JShape& S = a.s;
-  const int lane = threadIdx.x & 63;
   const long long nwaves = (long long)gridDim.x * (kCos2Threads / 64);
   const long long wid = (long long)blockIdx.x * (kCos2Threads / 64) + (threadIdx.x >> 6);
   const int per = S.cols + S.rows;

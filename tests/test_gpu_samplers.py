@@ -81,6 +81,45 @@ def test_sample_matches_oracle(name, B, nv, first):
     assert (_h(o["enc_noise"]) == want["enc_noise"]).all()
 
 
+def _iv_low16(seed):
+    """low 16 bits of a UniformSampler's IV = SHA-384(seed)[32:48] (big-endian counter)"""
+    return int.from_bytes(hashlib.sha384(seed).digest()[46:48], "big")
+
+
+def _seed_with_iv_low(lo, hi, tag):
+    for i in range(1 << 22):
+        s = hashlib.sha256(tag + i.to_bytes(4, "little")).digest()
+        if lo <= _iv_low16(s) <= hi:
+            return s
+    raise AssertionError("no seed found")
+
+
+@pytest.mark.parametrize("lo,hi", [(0xFF81, 0xFFFF), (0xFF70, 0xFF80), (0, 0x7F)])
+def test_cdt_counter_prefix_boundary(lo, hi):
+    """cdt2_noise_kernel's counter-mode caching (csprng.hpp aes_prefix) serves a polynomial's 128
+    blocks when its window start's low 16 counter bits leave room for them without a carry, and
+    the plain AES otherwise.  The window start's low 24 bits are the IV's, so the seed decides:
+    an IV straddling the boundary (>= 0xFF81: plain path), one that just fits (<= 0xFF80) and a
+    small one, each bit-exact against the oracle."""
+    import dataclasses
+
+    import torch
+    name, B, nv, first = "t10_b8", 3, 700, 11
+    P = PARAMS[name]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    prv = jindo.NewProver(params, b"Jindo!")
+    v = np.stack([make_v(q, nv, seed=41 + b) for b in range(B)])
+    seeds = dataclasses.replace(_seeds(b"prefix"), enc_cdt=_seed_with_iv_low(lo, hi, b"iv-%d" % lo))
+    sh = params.shapes(B)
+    o = {k: torch.zeros(sh[k], dtype=torch.int64, device="cuda") for k in ("last_row", "mask", "enc_noise", "mlwe_noise")}
+    prv.sample_dev(B, _t(v), nv, seeds, first, o["last_row"], o["mask"], o["enc_noise"], o["mlwe_noise"])
+    torch.cuda.synchronize()
+    want = co.CJindo(P, q).sample([P[k] for k in SD_KEYS], pyref.delta_inv(P["base"], P["exp"]), seeds.raw(), first, v)
+    assert (_h(o["enc_noise"]) == want["enc_noise"]).all()
+    assert (_h(o["mlwe_noise"]) == want["mlwe_noise"]).all()
+
+
 def test_commit_sampled_end_to_end():
     """rg_jindo_commit_sampled_dev == rg_jindo_commit_dev on rg_jindo_sample_dev's draws == the
     C oracle's commit on the C oracle's draws."""
