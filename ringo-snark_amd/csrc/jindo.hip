@@ -54,6 +54,7 @@ struct RnsPrime {
   uint64_t one_sh;           // floor(2^64 / q): x mod q = shoup(x, 1)
   uint64_t ninv, ninv_sh;    // d^-1 mod q
   uint64_t bmod, bmod_sh;    // base mod q
+  uint64_t rw1, rw1_sh;      // 2^64 w1 mod q, w1 = the forward table's first-stage root (prep256 stage 0)
 };
 
 struct RingDev {
@@ -383,7 +384,7 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
-template <int RK, int LO, int PAT>
+template <int RK, int LO, int PAT, int SP0 = 0>
 __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, uint64_t q, uint64_t q2,
                                            uint32_t t) {
   auto xof = [&](int rho) -> uint32_t {
@@ -393,7 +394,7 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
   };
   constexpr int NPK = 1 << RK;
 #pragma unroll
-  for (int sp = 0; sp < RK; ++sp) {
+  for (int sp = SP0; sp < RK; ++sp) {
     const int bw = RK - 1 - sp, b = LO + bw, k = 7 - b, half = 1 << bw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -403,8 +404,7 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
       // Harvey with a 4q-wide twiddle product: values in [0, 8q) (ring primes < 2^61), x
       // reduced to [0, 4q), t = y w - Q' q in [0, 4q) with Q' the Shoup quotient less the low
       // cross products (Q - 2 <= Q' <= Q): three 32-bit multiplies for the quotient, not four
-      uint64_t x = e[rho0];
-      x = x >= q2 ? x - q2 : x;  // q2 = 4q here
+      const uint64_t x = canon_x(e[rho0], q2);  // x >= 4q ? x - 4q : x, on the borrow (q2 = 4q here)
       const uint64_t y = e[rho0 + half];
       const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32), p0 = (uint32_t)w.y, p1 = (uint32_t)(w.y >> 32);
       const uint64_t qa = mad64(y1, p1, __umulhi(y1, p0)) + __umulhi(y0, p1);
@@ -413,6 +413,13 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
       e[rho0 + half] = x + q2 - tt;
     }
   }
+}
+
+// y w mod q in [0, 3q) for any 64-bit y: prep_round's Shoup product with the 3-multiply quotient
+__device__ __forceinline__ uint64_t shoup3(uint64_t y, uint64_t w, uint64_t wp, uint64_t q) {
+  const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32), p0 = (uint32_t)wp, p1 = (uint32_t)(wp >> 32);
+  const uint64_t qa = mad64(y1, p1, __umulhi(y1, p0)) + __umulhi(y0, p1);
+  return y * w - qa * q;
 }
 
 // signed integer -> residue in [0, q) without division (Shoup by 1 reduces any 64-bit value)
@@ -428,7 +435,9 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
   extern __shared__ ulonglong2 tw_lds[];  // the nq limbs' forward tables (w, w'), [nq][256]: dynamic LDS
   const JShape& S = a.s;
   const int nq = S.nq;
-  for (int i = threadIdx.x; i < nq * 256; i += blockDim.x) tw_lds[i] = a.R.fwd[i];
+  // slot 0 of each limb's table (unused by the transform) holds (2^64 w1, Shoup) for stage 0
+  for (int i = threadIdx.x; i < nq * 256; i += blockDim.x)
+    tw_lds[i] = (i & 255) ? a.R.fwd[i] : make_ulonglong2(a.R.p[i >> 8].rw1, a.R.p[i >> 8].rw1_sh);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
   const int wv = threadIdx.x >> 6;
@@ -464,41 +473,58 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     const ulonglong2* roots = tw_lds + lc * 256;
     // The encode tail MForm(dg) + MForm(+-s') - MForm(s) b (encoder.go:184-199) is MForm of ONE
     // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
-    // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  Inputs are (re)read per
-    // limb pair rather than held across the NTT.
+    // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  MForm is a factor 2^64 on
+    // every coefficient, so it rides on NTT stage 0: e holds v mod q (one add when |v| < q), and
+    // stage 0 multiplies by 2^64 and 2^64 w1 instead of w1.  Inputs are (re)read per limb pair
+    // rather than held across the NTT.
     uint64_t e[8];
-    uint32_t big = 0;  // bit y: coefficient t + 32 y needs the term-by-term form
+    uint32_t big = 0;  // bit y: coefficient t + 32 y takes the term-by-term reduction
 #pragma unroll
     for (int y = 0; y < 8; ++y) {
       const int k = (int)t + 32 * y;
       const long long c = nz[k];
       long long v = c;
+      bool ok = true;
       if (is_enc) {
         const int ks = k - S.slots;
         const long long cs = ks >= 0 ? nz[ks] : nz[ks + 256];
         const uint64_t s2 = k < S.slots ? 0ull - (uint64_t)cs : (uint64_t)cs;  // wrapped coefficients negate
-        const bool ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
-        big |= ok ? 0u : (1u << y);
+        ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
         v = (long long)((uint64_t)dg[k] + s2 - (uint64_t)c * S.base);
       }
-      const uint64_t av = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-      const uint64_t m = sh_mul(av, P.r64, P.r64_sh, q);  // Shoup: exact for any 64-bit input
-      e[y] = v < 0 ? mod_neg(m, q) : m;
+      const uint64_t r = v < 0 ? (uint64_t)v + q : (uint64_t)v;  // v mod q when -q <= v < q
+      ok = ok && r < q;
+      big |= ok ? 0u : (1u << y);
+      e[y] = r;
     }
     if (big) {  // rare (huge injected noise): every term reduced separately, same residue
       for (int y = 0; y < 8; ++y) {
         if (!((big >> y) & 1u)) continue;
-        const int k = (int)t + 32 * y, ks = k - S.slots;
-        const uint64_t cm = red_signed(nz[k], P);
-        uint64_t s2 = red_signed(ks >= 0 ? nz[ks] : nz[ks + 256], P);
-        if (k < S.slots) s2 = mod_neg(s2, q);
-        uint64_t val = mod_add(sh_mul(dg[k], 1, P.one_sh, q), s2, q);
-        val = mod_sub(val, sh_mul(cm, P.bmod, P.bmod_sh, q), q);
-        e[y] = sh_mul(val, P.r64, P.r64_sh, q);
+        const int k = (int)t + 32 * y;
+        if (is_enc) {
+          const int ks = k - S.slots;
+          const uint64_t cm = red_signed(nz[k], P);
+          uint64_t s2 = red_signed(ks >= 0 ? nz[ks] : nz[ks + 256], P);
+          if (k < S.slots) s2 = mod_neg(s2, q);
+          const uint64_t val = mod_add(sh_mul(dg[k], 1, P.one_sh, q), s2, q);
+          e[y] = mod_sub(val, sh_mul(cm, P.bmod, P.bmod_sh, q), q);
+        } else {
+          e[y] = red_signed(nz[k], P);
+        }
       }
     }
-    // NTT: H round (stages 0-2), H->M, M round (3-5), M->L, L round (6-7), L->H, store
-    prep_round<3, 5, 0>(e, roots, q, q2, t);
+    {  // stage 0 (pairs y, y + 4 of the H pattern, root w1) times 2^64: inputs in [0, q), outputs
+       // in [0, 8q) like every later stage's
+      const ulonglong2 rw = roots[0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t xr = shoup3(e[j], P.r64, P.r64_sh, q), yr = shoup3(e[j + 4], rw.x, rw.y, q);
+        e[j] = xr + yr;
+        e[j + 4] = xr + q2 - yr;
+      }
+    }
+    // NTT: H round (stages 1-2; 0 above), H->M, M round (3-5), M->L, L round (6-7), L->H, store
+    prep_round<3, 5, 0, 1>(e, roots, q, q2, t);
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
     wave_lds_fence();
@@ -514,12 +540,8 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     prep_round<2, 0, 2>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {  // [0, 8q) -> [0, q)
-      uint64_t x = e[r];
-      x = x >= q2 ? x - q2 : x;
-      x = x >= 2 * q ? x - 2 * q : x;
-      lds[rL8 + r] = x >= q ? x - q : x;
-    }
+    for (int r = 0; r < 8; ++r)  // [0, 8q) -> [0, q)
+      lds[rL8 + r] = canon_x(canon_x(canon_x(e[r], q2), 2 * q), q);
     wave_lds_fence();
     if (active) {
       uint64_t* o = dst + (long long)limb * 256;
@@ -2798,6 +2820,8 @@ static rg_status make_ring(int d, const uint64_t* primes, int n, uint64_t base, 
       x = h_mulmod(x, psi, q);
       y = h_mulmod(y, psii, q);
     }
+    R.rw1 = h_mulmod(R.r64, f[(size_t)l * d + 1].x, q);
+    R.rw1_sh = h_shoup(R.rw1, q);
   }
   RG_TRY(fwd.upload(f.data(), f.size() * sizeof(ulonglong2)));
   RG_TRY(bwd.upload(b.data(), b.size() * sizeof(ulonglong2)));

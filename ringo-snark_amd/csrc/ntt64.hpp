@@ -262,7 +262,10 @@ template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int 
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
                                             uint32_t hi, uint32_t t) {
   constexpr int G0 = COL ? 0 : 8;
-  constexpr bool UNIFORM = (COL || RP) && PAT == 0;  // twiddle index independent of the lane
+  // twiddle index independent of the lane: the H round of COL / RP tiles.  (The M round of COL
+  // tiles is wave-uniform too, x >> (b + 1) depending on t >> 2 = tid >> 6 only, but scalar loads
+  // there measured no faster: their lgkmcnt waits also wait for the exchange's LDS traffic.)
+  constexpr bool UNIFORM = (COL || RP) && PAT == 0;
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
