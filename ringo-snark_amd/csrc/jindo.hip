@@ -1927,19 +1927,21 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order):
       // coefficient k reads digit (k + (i+1) slots) mod 256, added when that index wrapped
       double fp[4] = {0.0, 0.0, 0.0, 0.0};
+      // deltaInv through the constant address space: scalar loads (a plain global load here waits
+      // on vmcnt(0) every digit, as the kernel's stores defeat the no-clobber analysis)
+      const __attribute__((address_space(4))) double* dlt = (const __attribute__((address_space(4))) double*)a.delta;
+#pragma unroll 4
       for (int i = 0; i < S.exp; ++i) {
-        const double di = a.delta[i];
+        const double di = dlt[i];
         if (di == 0.0) continue;
         const int base = 4 * lane + (i + 1) * S.slots;
         const uint4 q = dl[(base & 255) >> 2];
         const uint32_t gv[4] = {q.x, q.y, q.z, q.w};
+        // slots % 4 == 0 (the launch condition) makes base a multiple of 4: base + h >= 256 for
+        // all four coefficients or for none, so one sign per digit; fp + (-di) g == fp - di g
+        const double sdi = base >= 256 ? di : -di;
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          if (base + h >= 256)
-            fp[h] = fp[h] + di * (double)gv[h];
-          else
-            fp[h] = fp[h] - di * (double)gv[h];
-        }
+        for (int h = 0; h < 4; ++h) fp[h] = fp[h] + sdi * (double)gv[h];
       }
       wave_lds_fence();  // the slot is rewritten for the next polynomial after these reads
       if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
@@ -2346,11 +2348,16 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
 #pragma clang fp contract(on)
 
 // thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
+constexpr int kMlweLdsTab = 512;  // mlweSampler's table in LDS up to this size (configs: 123 entries)
 __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
   __shared__ uint32_t key[kKeyWords];
+  __shared__ uint64_t mtab[kMlweLdsTab];
   aes_lds_fill(lds, a.te0);
   aes_key_fill(key, a.key[kDomMlweRnd]);
+  const bool tab_lds = a.cdt_mlwe.size <= kMlweLdsTab;  // else the binary search reads global memory
+  if (tab_lds)
+    for (int i = threadIdx.x; i < a.cdt_mlwe.size; i += blockDim.x) mtab[i] = a.cdt_mlwe.tables[i];
   __syncthreads();
   // grid-stride: a bounded grid fills the 64 KiB LDS tables once per workgroup, not once per 512 pairs
   for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.n_ml_pairs;
@@ -2365,8 +2372,16 @@ __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   if (col != S.cols) {  // mlweSampler.Sample(0): centre 0, one table, no float tail
     uint64_t w0, w1;
     ks_words(a.key[kDomMlweCdt], gpoly, (uint64_t)m, lds, w0, w1);
-    out[2 * m] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0) + a.cdt_mlwe.tail_lo;
-    out[2 * m + 1] = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1) + a.cdt_mlwe.tail_lo;
+    int64_t v0, v1;
+    if (tab_lds) {
+      v0 = cdt_search(mtab, a.cdt_mlwe.size, w0);
+      v1 = cdt_search(mtab, a.cdt_mlwe.size, w1);
+    } else {
+      v0 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0);
+      v1 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1);
+    }
+    out[2 * m] = v0 + a.cdt_mlwe.tail_lo;
+    out[2 * m + 1] = v1 + a.cdt_mlwe.tail_lo;
   } else {  // roundedSampler.Sample(0, maskMLWEStdDev)
     for (int h = 0; h < 2; ++h) {
       const int k = 2 * m + h;
