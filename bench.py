@@ -31,6 +31,7 @@ import argparse
 import hashlib
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -346,6 +347,9 @@ _SAMP = ("cdt_noise_kernel", "cdt_tail_kernel", "cosac_noise_kernel", "mlwe_nois
 LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("ntt256_pass",), "j14": _DET + _SAMP, "j16": _DET + _SAMP}
 
 
+_PROBE_KERNEL = re.compile(r"ntt16_pass<.*, [1-9][0-9]*>\(")  # PROBE != 0: rg_set_probe's measurement variants
+
+
 def line_counters(C, line, units_per_step, kernel_ms_per_step):
     """traffic (HBM bytes per unit) and the VALU issue block for one line, or None.  A Jindo
     line's profiled run executes injected steps (the deterministic kernels) and sampled steps
@@ -358,8 +362,8 @@ def line_counters(C, line, units_per_step, kernel_ms_per_step):
     mix = VALU_MIX.get("kernels", {}) if VALU_MIX.get("lib_sha256") == C.get("lib_sha256") else {}
     fetch = write = valu = cyc = 0.0
     for n, k in Lc["kernels"].items():
-        if not any(p in n for p in LINE_KERNELS[line]):
-            continue
+        if not any(p in n for p in LINE_KERNELS[line]) or _PROBE_KERNEL.search(n):
+            continue  # (the compute-floor probe's launches run in the same process: not the step)
         st = se.get(line, Lc["steps"])
         if any(p in n for p in _DET):
             st += se.get(line + "_injected", 0)
