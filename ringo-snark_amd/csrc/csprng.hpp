@@ -126,6 +126,47 @@ __device__ __forceinline__ void aes_ctr(const K& key, uint64_t nhi, uint64_t nlo
   out[3] = fin(s3, s0, s1, s2, key.rk(59));
 }
 
+// Two blocks of one key in lockstep: each round issues both blocks' 32 table lookups together
+// (twice the loads in flight of one block) and reads the round key once for both.
+template <class K>
+__device__ __forceinline__ void aes_ctr_x2(const K& key, uint64_t hi0, uint64_t lo0, uint64_t hi1, uint64_t lo1,
+                                           const uint32_t* lds, uint32_t o0[4], uint32_t o1[4]) {
+  const uint32_t l0 = (threadIdx.x & 31u) << 2, l1 = l0 | 0x80u;
+  const uint64_t ivlo = ((uint64_t)key.iv(2) << 32) | key.iv(3), ivhi = ((uint64_t)key.iv(0) << 32) | key.iv(1);
+  const uint64_t c0 = ivlo + lo0, c1 = ivlo + lo1;
+  const uint64_t h0 = ivhi + hi0 + (c0 < lo0 ? 1u : 0u), h1 = ivhi + hi1 + (c1 < lo1 ? 1u : 0u);
+  const uint32_t k0 = key.rk(0), k1 = key.rk(1), k2 = key.rk(2), k3 = key.rk(3);
+  uint32_t a0 = (uint32_t)(h0 >> 32) ^ k0, a1 = (uint32_t)h0 ^ k1, a2 = (uint32_t)(c0 >> 32) ^ k2, a3 = (uint32_t)c0 ^ k3;
+  uint32_t b0 = (uint32_t)(h1 >> 32) ^ k0, b1 = (uint32_t)h1 ^ k1, b2 = (uint32_t)(c1 >> 32) ^ k2, b3 = (uint32_t)c1 ^ k3;
+  auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kr) {
+    return xor3(te_b<3>(lds, a, l0), te_b<2>(lds, b, l1), ror32(xor3(te_b<1>(lds, c, l0), te_b<0>(lds, d, l1), kr), 16));
+  };
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    const uint32_t r0 = key.rkr(4 * r), r1 = key.rkr(4 * r + 1), r2 = key.rkr(4 * r + 2), r3 = key.rkr(4 * r + 3);
+    const uint32_t ta0 = col(a0, a1, a2, a3, r0), tb0 = col(b0, b1, b2, b3, r0);
+    const uint32_t ta1 = col(a1, a2, a3, a0, r1), tb1 = col(b1, b2, b3, b0, r1);
+    const uint32_t ta2 = col(a2, a3, a0, a1, r2), tb2 = col(b2, b3, b0, b1, r2);
+    const uint32_t ta3 = col(a3, a0, a1, a2, r3), tb3 = col(b3, b0, b1, b2, r3);
+    a0 = ta0; a1 = ta1; a2 = ta2; a3 = ta3;
+    b0 = tb0; b1 = tb1; b2 = tb2; b3 = tb3;
+  }
+  auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    const uint32_t ab = __builtin_amdgcn_perm(te_b<3>(lds, a, l0), te_b<2>(lds, b, l0), 0x06020C0Cu);
+    const uint32_t cd = __builtin_amdgcn_perm(te_b<1>(lds, c, l0), te_b<0>(lds, d, l0), 0x0C0C0602u);
+    return xor3(ab, cd, k);
+  };
+  const uint32_t f0 = key.rk(56), f1 = key.rk(57), f2 = key.rk(58), f3 = key.rk(59);
+  o0[0] = fin(a0, a1, a2, a3, f0);
+  o1[0] = fin(b0, b1, b2, b3, f0);
+  o0[1] = fin(a1, a2, a3, a0, f1);
+  o1[1] = fin(b1, b2, b3, b0, f1);
+  o0[2] = fin(a2, a3, a0, a1, f2);
+  o1[2] = fin(b2, b3, b0, b1, f2);
+  o0[3] = fin(a3, a0, a1, a2, f3);
+  o1[3] = fin(b3, b0, b1, b2, f3);
+}
+
 // The two little-endian u64 keystream words of block `off` of instance `inst`'s window, i.e. of
 // counter block IV + inst 2^24 + off.  inst 2^24 is formed in 128 bits (hi = inst >> 40): an
 // instance number up to 2^64 - 1 never wraps onto another instance's window (oracle.c uni_init).
@@ -142,6 +183,19 @@ __device__ __forceinline__ void ks_words(const K& key, uint64_t inst, uint64_t o
 __device__ __forceinline__ void ks_words(const AesKey& K, uint64_t inst, uint64_t off, const uint32_t* lds, uint64_t& w0,
                                          uint64_t& w1) {
   ks_words(ArgKey{K}, inst, off, lds, w0, w1);
+}
+
+// blocks off0 and off1 of one instance's window (ks_words for both, in lockstep)
+template <class K>
+__device__ __forceinline__ void ks_words_x2(const K& key, uint64_t inst, uint64_t off0, uint64_t off1,
+                                            const uint32_t* lds, uint64_t w[4]) {
+  const uint64_t wlo = inst << kWinShift, lo0 = wlo + off0, lo1 = wlo + off1, whi = inst >> (64 - kWinShift);
+  uint32_t a[4], b[4];
+  aes_ctr_x2(key, whi + (lo0 < wlo ? 1u : 0u), lo0, whi + (lo1 < wlo ? 1u : 0u), lo1, lds, a, b);
+  w[0] = (uint64_t)bswap32(a[0]) | ((uint64_t)bswap32(a[1]) << 32);
+  w[1] = (uint64_t)bswap32(a[2]) | ((uint64_t)bswap32(a[3]) << 32);
+  w[2] = (uint64_t)bswap32(b[0]) | ((uint64_t)bswap32(b[1]) << 32);
+  w[3] = (uint64_t)bswap32(b[2]) | ((uint64_t)bswap32(b[3]) << 32);
 }
 
 // word `p` of the Sample() stream of instance `inst` (uniform.go:64-82): chunk c = KS_0 ^ ... ^ KS_c

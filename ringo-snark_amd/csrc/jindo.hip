@@ -1952,8 +1952,7 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       const unsigned long long gpoly =
           a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
       uint64_t u[4];
-      ks_words(key, gpoly, (uint64_t)(2 * lane), lds, u[0], u[1]);
-      ks_words(key, gpoly, (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
+      ks_words_x2(key, gpoly, (uint64_t)(2 * lane), (uint64_t)(2 * lane + 1), lds, u);
       // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111).  Fast path: the guide bucket of u's
       // top byte in table c0 holds <= 3 entries and none shares u's high word, so the lower bound
       // is lo + #(entries below u) with no equality (three LDS word compares); and v0 <= jmax[c0],
