@@ -133,6 +133,16 @@ rg_status rg_poly_evaluate_dev(const rg_field* f, const uint64_t* d_p, size_t n,
                                uint64_t* d_scratch, void* stream);
 size_t rg_poly_evaluate_scratch_bytes(const rg_field* f, size_t n);
 rg_status rg_poly_evaluate(const rg_field* f, const uint64_t* p, size_t n, const uint64_t* x, uint64_t* out);
+/* CyclotomicEvaluator.ModSwitchTo(pOut, pBig, qBig) (cyclotomic.go:97-124) on n coefficients:
+ * pBig[i] as w little-endian words of a two's-complement integer ([n][w], |pBig[i]| < 2^(64w-1);
+ * Go's big.Int values, e.g. PolyToBigintCentered output), qBig as w words (host, 0 < qBig <
+ * 2^(64w-1)); out[i] = the reference's round(pBig[i] q / qBig) mod q (remainders above
+ * floor(qBig/2) round up) in Montgomery form ([n][L]).  w <= 8.  The rank check ("input size
+ * not consistent") and IsNTT = false stay with the caller. */
+rg_status rg_poly_modswitch_dev(const rg_field* f, size_t n, const uint64_t* d_pbig, size_t w, const uint64_t* qbig,
+                                uint64_t* d_out, void* stream);
+rg_status rg_poly_modswitch(const rg_field* f, size_t n, const uint64_t* pbig, size_t w, const uint64_t* qbig,
+                            uint64_t* out);
 
 /* ---- Buckler prover device work -------------------------------- */
 /* Encoder.EncodeTo / RandEncodeTo (buckler/encoder.go:32-54) of `batch` witness vectors:

@@ -138,6 +138,22 @@ def _find_root(p, t1, t2):
     raise ValueError("no root")
 
 
+def mod_switch(pbig, qbig, q):
+    """CyclotomicEvaluator.ModSwitchTo (math/bigpoly/cyclotomic.go:98-124) over Python ints, the
+    value SetBigInt receives per coefficient: c = p q; cRem = c mod qBig (big.Int Mod: Euclidean);
+    cRem -= qBig when cRem > qBig >> 1; c = (c - cRem) / qBig (exact); c mod q."""
+    half = qbig >> 1
+    out = []
+    for p in pbig:
+        c = int(p) * q
+        r = c % qbig
+        if r > half:
+            r -= qbig
+        c = (c - r) // qbig
+        out.append(c % q)
+    return out
+
+
 def cyclotomic_tables(F, N):
     """NewCyclotomicTransformer (ntt.go:153-203).  Returns (tw, twInv, rankInv) as Montgomery
     reps; tw[k] = psi^brv(k), twInv[k] = psi^-brv(k)."""

@@ -8,10 +8,13 @@
 //     reversals (out[k] = p[brv(((2 brv(k) + 1) idx mod 2N - 1) / 2)]);
 //   * Poly.Evaluate (poly.go:64-76): a Horner tree -- Horner over 64-coefficient chunks (one
 //     lane each) in x, then over 64-value chunks of those in x^64, ... down to one value; the
-//     same field element as the reference's single Horner pass.
+//     same field element as the reference's single Horner pass;
+//   * CyclotomicEvaluator.ModSwitchTo (cyclotomic.go:97-124): one lane per coefficient, the
+//     reference's big-integer rounding division in fixed multiword arithmetic (below).
 // All field arithmetic is the Montgomery form of field.hpp (gnark's representation), so every
 // output limb equals the reference's.
 #include <cstring>
+#include <vector>
 
 #include "common.hpp"
 #include "field.hpp"
@@ -215,6 +218,242 @@ static rg_status eval_L(const rg_field* f, const uint64_t* p, long long n, const
   }
 }
 
+// ---- ModSwitchTo ---------------------------------------------------------------------------
+// Per coefficient p (w words, two's complement; |p| < 2^(64w-1)), with c = p q:
+//   cRem = c mod qBig (Euclidean); cRem -= qBig when cRem > floor(qBig/2); c = (c - cRem) / qBig
+//   mod q (cyclotomic.go:111-121).
+// With A = |p| q = Qa qBig + ra (0 <= ra < qBig) this is
+//   p >= 0: M = Qa + [ra > floor(qBig/2)],   result M mod q
+//   p <  0: M = Qa + [ra >= qBig - floor(qBig/2)],   result (-M) mod q
+// (for p < 0, c mod qBig = qBig - ra unless ra = 0, and the rounding moves toward +inf).  Both
+// divisions are Barrett with host-computed reciprocals of 2^(64 nx), nx = w + L the width of A:
+// the estimate floor(x mu / 2^(64 nx)) is at most 2 below the quotient, fixed by at most two
+// subtractions.  Arrays are sized for w <= kMsMaxW.
+constexpr int kMsMaxW = 8;
+
+template <int L>
+struct MsArgs {
+  FieldParams<L> F;
+  uint64_t r2[L];                          // R^2 mod q (SetBigInt -> Montgomery form)
+  const uint64_t* in;                      // [n][w]
+  uint64_t* out;                           // [n][L]
+  long long n;
+  int w, nx, nmu1, nmu2;
+  uint64_t qbig[kMsMaxW];
+  uint64_t tpos[kMsMaxW], tneg[kMsMaxW];   // floor(qBig/2) + 1, qBig - floor(qBig/2)
+  uint64_t mu1[kMsMaxW + 16];              // floor(2^(64 nx) / qBig)
+  uint64_t mu2[kMsMaxW + 16];              // floor(2^(64 nx) / q)
+};
+
+// a >= b over n words (little-endian)
+__device__ __forceinline__ bool mw_geq(const uint64_t* a, const uint64_t* b, int n) {
+  for (int i = n - 1; i >= 0; --i)
+    if (a[i] != b[i]) return a[i] > b[i];
+  return true;
+}
+// a -= b over n words (a >= b)
+__device__ __forceinline__ void mw_sub(uint64_t* a, const uint64_t* b, int n) {
+  uint32_t br = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t x = a[i], y = b[i];
+    const uint64_t d = x - y - br;
+    br = (x < y || (x == y && br)) ? 1u : 0u;
+    a[i] = d;
+  }
+}
+// a (na words) >= b (nb words, nb <= na); a -= b with b zero-extended
+__device__ __forceinline__ bool mw_geq_ext(const uint64_t* a, int na, const uint64_t* b, int nb) {
+  for (int i = na - 1; i >= nb; --i)
+    if (a[i] != 0) return true;
+  return mw_geq(a, b, nb);
+}
+__device__ __forceinline__ void mw_sub_ext(uint64_t* a, int na, const uint64_t* b, int nb) {
+  uint32_t br = 0;
+  for (int i = 0; i < na; ++i) {
+    const uint64_t x = a[i], y = i < nb ? b[i] : 0;
+    a[i] = x - y - br;
+    br = (x < y || (x == y && br)) ? 1u : 0u;
+  }
+}
+// quo (nx words), rem (nm words) of x (nx words) by m (nm words, m > 0) with mu = floor(2^(64 nx) / m)
+// (nmu words); x and the scratch live in the caller's arrays
+template <int NX>
+__device__ void ms_divmod(const uint64_t* x, int nx, const uint64_t* m, int nm, const uint64_t* mu, int nmu,
+                          uint64_t* quo, uint64_t* rem) {
+  uint64_t pr[2 * NX + 1];
+  for (int i = 0; i < nx + nmu; ++i) pr[i] = 0;
+  for (int i = 0; i < nx; ++i) {  // pr = x mu
+    uint64_t carry = 0;
+    for (int j = 0; j < nmu; ++j) {
+      uint64_t lo, hi;
+      mul_wide(x[i], mu[j], lo, hi);
+      uint32_t c = 0;
+      lo = addc(lo, pr[i + j], c);
+      hi += c;
+      c = 0;
+      lo = addc(lo, carry, c);
+      hi += c;
+      pr[i + j] = lo;
+      carry = hi;
+    }
+    pr[i + nmu] = carry;
+  }
+  for (int i = 0; i < nx; ++i) quo[i] = i < nmu ? pr[nx + i] : 0;  // floor(x mu / 2^(64 nx)) < 2^(64 nx)
+  uint64_t r[NX + 1];  // x - quo m, exact in nx words
+  for (int i = 0; i < nx; ++i) r[i] = x[i];
+  for (int i = 0; i < nm; ++i) {  // r -= quo * m[i] << 64 i (low nx words)
+    uint64_t carry = 0;
+    uint32_t br = 0;
+    for (int j = 0; i + j < nx; ++j) {
+      uint64_t lo, hi;
+      mul_wide(quo[j], m[i], lo, hi);
+      uint32_t c = 0;
+      lo = addc(lo, carry, c);
+      hi += c;
+      carry = hi;
+      const uint64_t a = r[i + j];
+      const uint64_t d = a - lo - br;
+      br = (a < lo || (a == lo && br)) ? 1u : 0u;
+      r[i + j] = d;
+    }
+  }
+  for (int it = 0; it < 3 && mw_geq_ext(r, nx, m, nm); ++it) {  // at most two corrections
+    mw_sub_ext(r, nx, m, nm);
+    for (int i = 0; i < nx && ++quo[i] == 0; ++i) {
+    }
+  }
+  for (int i = 0; i < nm; ++i) rem[i] = i < nx ? r[i] : 0;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void modswitch_kernel(MsArgs<L> a) {
+  constexpr int NX = kMsMaxW + L;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.n) return;
+  const int w = a.w, nx = a.nx;
+  const uint64_t* pin = a.in + gid * w;
+  uint64_t mag[kMsMaxW];
+  const bool neg = (pin[w - 1] >> 63) != 0;
+  {
+    uint32_t c = neg ? 1u : 0u;  // |p| = (p ^ -neg) + neg
+    for (int i = 0; i < w; ++i) {
+      const uint64_t x = neg ? ~pin[i] : pin[i];
+      mag[i] = x + c;
+      c = (c && mag[i] == 0) ? 1u : 0u;
+    }
+  }
+  uint64_t A[NX];
+  for (int i = 0; i < nx; ++i) A[i] = 0;
+  for (int i = 0; i < w; ++i) {  // A = |p| q
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      uint64_t lo, hi;
+      mul_wide(mag[i], a.F.q[j], lo, hi);
+      uint32_t c = 0;
+      lo = addc(lo, A[i + j], c);
+      hi += c;
+      c = 0;
+      lo = addc(lo, carry, c);
+      hi += c;
+      A[i + j] = lo;
+      carry = hi;
+    }
+    A[i + L] = carry;
+  }
+  uint64_t Q[NX], ra[kMsMaxW];
+  ms_divmod<NX>(A, nx, a.qbig, w, a.mu1, a.nmu1, Q, ra);
+  if (mw_geq(ra, neg ? a.tneg : a.tpos, w))
+    for (int i = 0; i < nx && ++Q[i] == 0; ++i) {
+    }
+  uint64_t Qq[NX], r[L];
+  ms_divmod<NX>(Q, nx, a.F.q, L, a.mu2, a.nmu2, Qq, r);
+  bool nz = false;
+#pragma unroll
+  for (int j = 0; j < L; ++j) nz |= r[j] != 0;
+  if (neg && nz) {  // (-M) mod q = q - (M mod q)
+    uint64_t t[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) t[j] = a.F.q[j];
+    mw_sub(t, r, L);
+#pragma unroll
+    for (int j = 0; j < L; ++j) r[j] = t[j];
+  }
+  uint64_t o[L];
+  f_mul<L>(o, r, a.r2, a.F);  // SetBigInt: r R mod q
+  cp<L>(a.out + gid * L, o);
+}
+
+// host: floor(2^(64 nx) / m) by restoring binary division (m: nm words, result <= nx + 1 words)
+static int host_recip(const uint64_t* m, int nm, int nx, uint64_t* mu, int cap) {
+  const int nq = nx + 1;
+  if (nq > cap) return -1;
+  std::vector<uint64_t> r(nm + 1, 0);
+  for (int i = 0; i < nq; ++i) mu[i] = 0;
+  auto geq = [&](void) {
+    if (r[nm] != 0) return true;
+    for (int i = nm - 1; i >= 0; --i)
+      if (r[i] != m[i]) return r[i] > m[i];
+    return true;
+  };
+  for (int bit = 64 * nx; bit >= 0; --bit) {  // dividend 2^(64 nx): a single 1 bit at position 64 nx
+    for (int i = nm; i > 0; --i) r[i] = (r[i] << 1) | (r[i - 1] >> 63);  // r = 2 r + bit
+    r[0] = (r[0] << 1) | (bit == 64 * nx ? 1u : 0u);
+    if (geq()) {
+      uint64_t br = 0;
+      for (int i = 0; i <= nm; ++i) {
+        const uint64_t y = i < nm ? m[i] : 0;
+        const uint64_t x = r[i];
+        r[i] = x - y - br;
+        br = (x < y || (x == y && br)) ? 1u : 0u;
+      }
+      mu[bit >> 6] |= 1ull << (bit & 63);
+    }
+  }
+  int n = nq;
+  while (n > 1 && mu[n - 1] == 0) --n;
+  return n;
+}
+
+template <int L>
+static rg_status modswitch_L(const rg_field* f, const uint64_t* pbig, int w, const uint64_t* qbig, uint64_t* out,
+                             long long n, hipStream_t st) {
+  MsArgs<L> a;
+  memset(&a, 0, sizeof(a));
+  memcpy(a.F.q, f->q, 8 * L);
+  a.F.qinv = f->qinv;
+  memcpy(a.r2, f->r2, 8 * L);
+  a.in = pbig;
+  a.out = out;
+  a.n = n;
+  a.w = w;
+  a.nx = w + L;
+  memcpy(a.qbig, qbig, 8 * w);
+  // thresholds: h = floor(qBig / 2); tpos = h + 1, tneg = qBig - h
+  uint64_t h[kMsMaxW];
+  for (int i = 0; i < w; ++i) h[i] = (qbig[i] >> 1) | (i + 1 < w ? (qbig[i + 1] << 63) : 0);
+  {
+    uint32_t c = 1;
+    for (int i = 0; i < w; ++i) {
+      a.tpos[i] = h[i] + c;
+      c = (c && a.tpos[i] == 0) ? 1u : 0u;
+    }
+    uint64_t br = 0;
+    for (int i = 0; i < w; ++i) {
+      const uint64_t x = qbig[i], y = h[i];
+      a.tneg[i] = x - y - br;
+      br = (x < y || (x == y && br)) ? 1u : 0u;
+    }
+  }
+  int nqb = w;
+  while (nqb > 1 && qbig[nqb - 1] == 0) --nqb;
+  a.nmu1 = host_recip(qbig, nqb, a.nx, a.mu1, kMsMaxW + 16);
+  a.nmu2 = host_recip(f->q, L, a.nx, a.mu2, kMsMaxW + 16);
+  if (a.nmu1 < 0 || a.nmu2 < 0) return RG_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(modswitch_kernel<L>, dim3(grid_of(n)), dim3(256), 0, st, a);
+  return check_launch("modswitch");
+}
+
 #define RG_DISPATCH_L(L_, CALL)                 \
   switch (L_) {                                 \
     case 1: return CALL(1);                     \
@@ -277,6 +516,19 @@ rg_status rg_poly_evaluate_dev(const rg_field* f, const uint64_t* d_p, size_t n,
 #undef RG_EV
 }
 
+rg_status rg_poly_modswitch_dev(const rg_field* f, size_t n, const uint64_t* d_pbig, size_t w, const uint64_t* qbig,
+                                uint64_t* d_out, void* stream) {
+  if (!f || !qbig || w == 0 || w > (size_t)kMsMaxW || (n && (!d_pbig || !d_out))) return RG_ERR_INVALID;
+  bool qz = true;
+  for (size_t i = 0; i < w; ++i) qz = qz && qbig[i] == 0;
+  if (qz || (qbig[w - 1] >> 63)) return RG_ERR_INVALID;  // qBig > 0, as a w-word signed value
+  if (n == 0) return RG_OK;
+  hipStream_t st = as_stream(stream);
+#define RG_MS(L) modswitch_L<L>(f, d_pbig, (int)w, qbig, d_out, (long long)n, st)
+  RG_DISPATCH_L(f->L, RG_MS)
+#undef RG_MS
+}
+
 size_t rg_poly_evaluate_scratch_bytes(const rg_field* f, size_t n) {
   return f ? (2 * ((n + kEvalChunk - 1) / kEvalChunk) + 2) * f->L * 8 : 0;
 }
@@ -305,6 +557,18 @@ rg_status rg_poly_aut(const rg_field* f, size_t rank, long long idx, int ntt_dom
   RG_TRY(dq.alloc(bytes));
   RG_TRY(rg_poly_aut_dev(f, rank, idx, ntt_domain, dq.as<uint64_t>(), dp.as<uint64_t>(), 1, nullptr));
   RG_HIP(hipMemcpy(out, dq.p, bytes, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+
+rg_status rg_poly_modswitch(const rg_field* f, size_t n, const uint64_t* pbig, size_t w, const uint64_t* qbig,
+                            uint64_t* out) {
+  if (!f || !qbig || (n && (!pbig || !out)) || w == 0 || w > (size_t)kMsMaxW) return RG_ERR_INVALID;
+  if (n == 0) return rg_poly_modswitch_dev(f, 0, nullptr, w, qbig, nullptr, nullptr);
+  DevBuf dp, dq;
+  RG_TRY(dp.upload(pbig, n * w * 8));
+  RG_TRY(dq.alloc(n * f->L * 8));
+  RG_TRY(rg_poly_modswitch_dev(f, n, dp.as<uint64_t>(), w, qbig, dq.as<uint64_t>(), nullptr));
+  RG_HIP(hipMemcpy(out, dq.p, n * f->L * 8, hipMemcpyDeviceToHost));
   return RG_OK;
 }
 

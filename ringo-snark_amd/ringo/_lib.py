@@ -72,6 +72,8 @@ _SIGS = {
     "rg_poly_evaluate_dev": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, vp, vp]),
     "rg_poly_evaluate_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
     "rg_poly_evaluate": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u64p, u64p]),
+    "rg_poly_modswitch_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_size_t, u64p, vp, vp]),
+    "rg_poly_modswitch": (ctypes.c_int, [vp, ctypes.c_size_t, u64p, ctypes.c_size_t, u64p, u64p]),
     "rg_buckler_encode_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp, vp]),
     "rg_buckler_encode_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
     "rg_buckler_encode": (ctypes.c_int, [vp, ctypes.c_size_t, u64p, u64p, u64p]),

@@ -375,6 +375,31 @@ class CyclotomicEvaluator(_BaseOperator):
         pOut.IsNTT = p.IsNTT
 
 
+    def ModSwitch(self, pBig, qBig):  # cyclotomic.go:91-96
+        o = self.NewPoly(False)
+        self.ModSwitchTo(o, pBig, qBig)
+        return o
+
+    def ModSwitchTo(self, pOut, pBig, qBig):  # cyclotomic.go:98-124
+        """pBig: rank Python ints (any sign, e.g. PolyToBigintCentered output), qBig > 0: each
+        coefficient to round(p q / qBig) mod q (rg_poly_modswitch), pOut in the coefficient domain."""
+        if len(pBig) != self.rank:
+            raise RingoPanic("input size not consistent")
+        qBig = int(qBig)
+        if qBig <= 0:
+            raise RingoPanic("qBig must be positive")
+        bits = max([qBig.bit_length()] + [abs(int(x)).bit_length() for x in pBig]) + 1  # + sign bit
+        w = (bits + 63) // 64
+        if w > 8:
+            raise RingoPanic("ModSwitch: operands wider than 511 bits are not supported")
+        mask = (1 << (64 * w)) - 1
+        words = np.array([[((int(x) & mask) >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(w)] for x in pBig],
+                         dtype=np.uint64).reshape(self.rank, w)
+        qw = np.array([(qBig >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(w)], dtype=np.uint64)
+        check(lib().rg_poly_modswitch(self.field.h, self.rank, ptr(words), w, ptr(qw), ptr(pOut.Coeffs)))
+        pOut.IsNTT = False
+
+
 class CyclicEvaluator(_BaseOperator):
     """NewCyclicEvaluator (cyclic.go:11-16)."""
 

@@ -1,5 +1,6 @@
 """GPU parity: the remaining bigpoly operators (rg_poly_*: QuoRemByVanishing cyclic.go:18-37,
-AutTo cyclotomic.go:29-86, Poly.Evaluate poly.go:64-76) vs the C oracle, bit-exact, through the
+AutTo cyclotomic.go:29-86, Poly.Evaluate poly.go:64-76, ModSwitchTo cyclotomic.go:97-124) vs the C
+oracle (ModSwitch: vs pyref.mod_switch's big-integer restatement), bit-exact, through the
 Python mirror of the reference's evaluators (host entry points) and the batched device forms."""
 import numpy as np
 import pytest
@@ -100,3 +101,33 @@ def test_batched_device_forms(fields):
     check(lib().rg_poly_quorem_vanishing_dev(F.h, rank, N, quo.data_ptr(), d.data_ptr(), d.data_ptr(), B, None))
     torch.cuda.synchronize()
     assert torch.equal(d, rem)
+
+
+@pytest.mark.parametrize("key", ["p63", "mult_zp", "bfv_zp", "jindo_zp", "zp440", "zp880"])
+@pytest.mark.parametrize("qbits", [2, 62, 64, 130, 255, 300, 509])
+def test_mod_switch(fields, key, qbits):
+    """CyclotomicEvaluator.ModSwitch on centred inputs (the bfv example's PolyToBigintCentered,
+    examples/bfv/main.go:152-155), the range ends, exact ties and values beyond qBig."""
+    import pyref
+    q = fields[key]
+    F = ringo.Field(q)
+    rank = 1 << 10
+    rng = np.random.default_rng(qbits)
+    qbig = (int.from_bytes(rng.bytes(64), "little") % (1 << qbits)) | (1 << (qbits - 1)) | (qbits & 1)
+    ps = [int.from_bytes(rng.bytes(72), "little") % qbig - (qbig >> 1) for _ in range(rank)]
+    edge = [0, 1, -1, qbig - 1, -(qbig - 1), qbig >> 1, -(qbig >> 1), (qbig + 1) >> 1, -((qbig + 1) >> 1),
+            3 * qbig + 5, -(3 * qbig) - 1]
+    ps[:len(edge)] = edge
+    ev = ringo.NewCyclotomicEvaluator(F, rank)
+    out = ev.ModSwitch(ps, qbig)
+    assert not out.IsNTT
+    rinv = pow(1 << (64 * F.L), -1, q)
+    got = [x * rinv % q for x in co.from_limbs(out.Coeffs)]
+    assert got == pyref.mod_switch(ps, qbig, q)
+
+
+def test_mod_switch_panics(fields):
+    F = ringo.Field(fields["p63"])
+    ev = ringo.NewCyclotomicEvaluator(F, 64)
+    with pytest.raises(RingoPanic, match="input size not consistent"):
+        ev.ModSwitch([1] * 63, 97)

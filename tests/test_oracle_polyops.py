@@ -5,7 +5,9 @@ pinned by the mathematics they implement, independently of the loops:
   * NTT(Aut_idx(p)) = Aut_idx(NTT(p)) between the coefficient and NTT-domain paths, through the
     oracle's negacyclic transform (itself pinned in test_oracle.py), and Aut is the ring map
     X -> X^idx of Z_q[X]/(X^N + 1) (checked on monomials);
-  * Evaluate = sum p_i x^i in Python integers (Montgomery representatives in and out)."""
+  * Evaluate = sum p_i x^i in Python integers (Montgomery representatives in and out);
+  * ModSwitch (pyref.mod_switch, cyclotomic.go:98-124) = ceil(p q / qBig - 1/2) mod q in exact
+    rationals: the reference's remainder rule is round-half-down, for either sign of p."""
 import numpy as np
 import pytest
 
@@ -75,4 +77,22 @@ def test_evaluate_is_sum_of_powers(fields, key, n):
     xv = co.from_limbs(x)[0] * rinv % q
     want = sum(c * rinv % q * pow(xv, i, q) for i, c in enumerate(co.from_limbs(p) if n else [])) % q
     got = co.from_limbs(cf.evaluate(p if n else np.zeros((0, cf.L), np.uint64), x)[None])[0] * rinv % q
+    assert got == want
+
+
+@pytest.mark.parametrize("key", ["p63", "bfv_zp", "jindo_zp"])
+@pytest.mark.parametrize("qbig", [2, 3, 2**61 - 1, 2**64, 3 * 2**100 + 7, 2**300 - 2**17, 2**511 - 1])
+def test_mod_switch_is_round_half_down(fields, key, qbig):
+    from fractions import Fraction
+    import math
+
+    import pyref
+    q = fields[key]
+    rng = np.random.default_rng(qbig % 1000)
+    ps = [0, 1, -1, qbig - 1, -(qbig - 1), qbig >> 1, -(qbig >> 1), (qbig + 1) >> 1, -((qbig + 1) >> 1)]
+    ps += [int.from_bytes(rng.bytes(72), "little") % qbig - (qbig >> 1) for _ in range(40)]
+    if qbig % 2 == 0:  # exact ties p q = (k + 1/2) qBig, when q is odd
+        ps += [(qbig // 2) * pow(q, -1, qbig) % qbig] if math.gcd(q, qbig) == 1 else []
+    got = pyref.mod_switch(ps, qbig, q)
+    want = [math.ceil(Fraction(p * q, qbig) - Fraction(1, 2)) % q for p in ps]
     assert got == want
