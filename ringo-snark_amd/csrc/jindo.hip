@@ -1568,8 +1568,16 @@ __global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
 //                       per sample (cdt_noise_kernel + cdt_tail_kernel: the round-2 form, kept
 //                       behind RINGO_CDT=legacy);
 //   cosac2_noise_kernel COSAC groups as a work queue through one state machine.
+// profiling variants' stand-in keystream (never in a production build)
+__device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 #ifndef RG_VAR
-#define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC)
+#define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC),
+                  // 16 no AES in cosac2, 32 no AES in cdt2 (keystream replaced by a SplitMix64 hash)
 #endif
 #pragma clang fp contract(off)
 constexpr int kCdtWaves = 16;       // waves per cdt_noise_kernel workgroup (one workgroup per CU)
@@ -1902,6 +1910,11 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   const double two_s2 = 2.0 * C.sigma * C.sigma;
   const LdsKey key{keyl};
   const int sstride = n + 2;
+  // deltaInv through the constant address space: scalar loads (a plain global load waits on
+  // vmcnt(0) per digit, as the kernel's stores defeat the no-clobber analysis)
+  const __attribute__((address_space(4))) double* dlt = (const __attribute__((address_space(4))) double*)a.delta;
+  int i0 = 0;  // first nonzero deltaInv
+  while (i0 < S.exp && dlt[i0] == 0.0) ++i0;
   for (long long p0 = ((long long)blockIdx.x * kCdt2Waves + wl) * kCdtChunk; p0 < npoly; p0 += nw * kCdtChunk) {
     const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
     int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
@@ -1927,22 +1940,29 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order):
       // coefficient k reads digit (k + (i+1) slots) mod 256, added when that index wrapped
       double fp[4] = {0.0, 0.0, 0.0, 0.0};
-      // deltaInv through the constant address space: scalar loads (a plain global load here waits
-      // on vmcnt(0) every digit, as the kernel's stores defeat the no-clobber analysis)
-      const __attribute__((address_space(4))) double* dlt = (const __attribute__((address_space(4))) double*)a.delta;
-#pragma unroll 4
-      for (int i = 0; i < S.exp; ++i) {
-        const double di = dlt[i];
-        if (di == 0.0) continue;
-        const int base = 4 * lane + (i + 1) * S.slots;
-        const uint4 q = dl[(base & 255) >> 2];
-        const uint32_t gv[4] = {q.x, q.y, q.z, q.w};
+      // Leading zero deltas (12 of 16 at the configs' shapes: b^i / p underflows the double
+      // grid) are skipped once per kernel (i0); later zeros are added: fp starts at +0 and never
+      // becomes -0, so adding 0 * g changes nothing, and four digits' loads are in flight at once.
+      auto cstep = [&](double di, int i, const uint4& q) {
         // slots % 4 == 0 (the launch condition) makes base a multiple of 4: base + h >= 256 for
         // all four coefficients or for none, so one sign per digit; fp + (-di) g == fp - di g
-        const double sdi = base >= 256 ? di : -di;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) fp[h] = fp[h] + sdi * (double)gv[h];
+        const double sdi = 4 * lane + (i + 1) * S.slots >= 256 ? di : -di;
+        fp[0] = fp[0] + sdi * (double)q.x;
+        fp[1] = fp[1] + sdi * (double)q.y;
+        fp[2] = fp[2] + sdi * (double)q.z;
+        fp[3] = fp[3] + sdi * (double)q.w;
+      };
+      auto dslot = [&](int i) { return dl[((4 * lane + (i + 1) * S.slots) & 255) >> 2]; };
+      int i = i0;
+      for (; i + 4 <= S.exp; i += 4) {
+        const uint4 q0 = dslot(i), q1 = dslot(i + 1), q2 = dslot(i + 2), q3 = dslot(i + 3);
+        const double d0 = dlt[i], d1 = dlt[i + 1], d2 = dlt[i + 2], d3 = dlt[i + 3];
+        cstep(d0, i, q0);
+        cstep(d1, i + 1, q1);
+        cstep(d2, i + 2, q2);
+        cstep(d3, i + 3, q3);
       }
+      for (; i < S.exp; ++i) cstep(dlt[i], i, dslot(i));
       wave_lds_fence();  // the slot is rewritten for the next polynomial after these reads
       if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
         reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
@@ -1952,7 +1972,11 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       const unsigned long long gpoly =
           a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
       uint64_t u[4];
+#if RG_VAR & 32
+      for (int h = 0; h < 4; ++h) u[h] = var_mix64(gpoly * 0x9E3779B97F4A7C15ull + 4u * lane + h);
+#else
       ks_words_x2(key, gpoly, (uint64_t)(2 * lane), (uint64_t)(2 * lane + 1), lds, u);
+#endif
       // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111).  Fast path: the guide bucket of u's
       // top byte in table c0 holds <= 3 entries and none shares u's high word, so the lower bound
       // is lo + #(entries below u) with no equality (three LDS word compares); and v0 <= jmax[c0],
@@ -2311,7 +2335,12 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
         const LdsKey k{keys + s * kCos2KeyStride};
         if (p < 1024) {
           uint64_t w1;
+#if RG_VAR & 16
+          w = var_mix64(inst * 0x9E3779B97F4A7C15ull + 2u * p + 1315423911u * s);
+          w1 = var_mix64(w);
+#else
           ks_words(k, inst, p / 2, lds, w, w1);
+#endif
           if (s)
             L.spare[1] = w1;
           else
