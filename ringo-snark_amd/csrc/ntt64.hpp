@@ -239,6 +239,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_buf(const void* p) {
 #ifndef RG_NTT_AUX
 #define RG_NTT_AUX 2  // cache policy of the transform's data loads / stores: nt (measured -3% per step vs 0, sc1 no better)
 #endif
+#ifndef RG_NTT_LTW
+#define RG_NTT_LTW 1  // L-round twiddles staged in LDS per tile (COL, RP); 0 = per-lane global loads
+#endif
 #ifndef RG_NTT_SAUX
 #define RG_NTT_SAUX RG_NTT_AUX
 #endif
@@ -258,9 +261,12 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 // 4 = no global data loads / stores (the tile is synthesised from the thread index and its
 // result kept live by a store that never fires): the compute floor (butterflies, twiddle loads,
 // LDS exchanges) of the same launch, timed by bench.py through rg_set_probe
+// LTW: the L round (PAT 2) reads its twiddles from the tile's LDS copy `ltw` (192 entries staged
+// by ntt16_tile: COL tw[64, 256), RP the row's lane-ordered copy) instead of per-lane global loads
 template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
-                                            uint32_t hi, uint32_t t) {
+                                            uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr) {
+  constexpr bool LTW = PAT == 2 && (COL || RP) && RG_NTT_LTW;
   constexpr int G0 = COL ? 0 : 8;
   // twiddle index independent of the lane: the H round of COL / RP tiles.  (The M round of COL
   // tiles is wave-uniform too, x >> (b + 1) depending on t >> 2 = tid >> 6 only, but scalar loads
@@ -301,6 +307,14 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
         const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
         const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
         const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[iu];
+        w[j] = v.x;
+        wp[j] = v.y;
+      } else if constexpr (LTW && COL) {
+        const ulonglong2 v = ltw[(1u << k) + (xof(rho0) >> (b + 1)) - 64u];
+        w[j] = v.x;
+        wp[j] = v.y;
+      } else if constexpr (LTW) {
+        const ulonglong2 v = ltw[(k == 6 ? 32u * grp : 64u + 32u * (rho0 >> 1)) + t];
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (!COL && PAT == 2) {
@@ -344,7 +358,7 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
 // Every pattern pair was checked conflict-free for ds_*_b64 half-wave groups
 // (SQ_LDS_BANK_CONFLICT = 0 for COL in profiles/r01_ntt16_pmc_summary.txt).
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0>
-__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds) {
+__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw) {
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
@@ -360,6 +374,12 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
+  constexpr bool LTW = (COL || RP) && RG_NTT_LTW && (PROBE & 1) == 0;
+  if constexpr (LTW) {  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads)
+    const uint32_t base = COL ? 64u : 65536u + hi * 192u;
+    if (tid < 384u)
+      reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
+  }
   // ---- global load
   if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
@@ -407,7 +427,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[COL ? bL + 16 * r : rL9 + r];
-    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     if (CANON) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
@@ -434,7 +454,8 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
       for (int r = 0; r < 8; ++r) e[r] = lds[rL8 + r];
       __syncthreads();
     }
-    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
+    if constexpr (COL && LTW) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
+    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     // exchange L -> M
 #pragma unroll
     for (int r = 0; r < 8; ++r) lds[COL ? bL + 16 * r : rL9 + r] = e[r];
@@ -469,7 +490,8 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP = false, int MINW = 1, int PROBE = 0>
 __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
   __shared__ uint64_t lds[16 * 288];
-  ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds);
+  __shared__ ulonglong2 ltw[(COL || RP) && RG_NTT_LTW ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
+  ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds, ltw);
 }
 
 #endif  // __HIPCC__
