@@ -1577,7 +1577,8 @@ __device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
 }
 #ifndef RG_VAR
 #define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC),
-                  // 16 no AES in cosac2, 32 no AES in cdt2 (keystream replaced by a SplitMix64 hash)
+                  // 16 no AES in cosac2, 32 no AES in cdt2 (keystream replaced by a SplitMix64 hash),
+                  // 64 cosac2 without libm exp / log (cheap stand-ins: cost of the rare branches)
 #endif
 #pragma clang fp contract(off)
 constexpr int kCdtWaves = 16;       // waves per cdt_noise_kernel workgroup (one workgroup per CU)
@@ -2164,6 +2165,13 @@ struct Cos2Lane {
 //          (1 + 2^-50) <= arg (the product form of the quotient, its rounding covered by the
 //          2^-50) and exp(arg) >= 1 + arg (exp within an ulp, covered by the 2^-48); else the
 //          reference's division and exp decide.
+#if RG_VAR & 64
+#define RG_COS_EXP(x) (1.0 + (x))
+#define RG_COS_LOG(x) ((x) - 1.0)
+#else
+#define RG_COS_EXP(x) exp(x)
+#define RG_COS_LOG(x) log(x)
+#endif
 template <class Z>
 __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, const double* sdv, long long* en) {
   const double rn = 3.442619855899;
@@ -2204,7 +2212,7 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
     if (!acc) {
       const double ap = -D * sdv[4 * code + 1] * (1.0 + 8.881784197001252e-16);  // a' <= arg < 0
       acc = fw < (1.0 + ap) * 0.99999999999999644729;
-      if (!acc) acc = fw < exp(-D / (2.0 * sdv[4 * code] * sdv[4 * code]));
+      if (!acc) acc = fw < RG_COS_EXP(-D / (2.0 * sdv[4 * code] * sdv[4 * code]));
     }
     if (acc) {
       en[L.oi] = (long long)L.y_round + (long long)L.c_int;
@@ -2216,7 +2224,7 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
     nst = kCoNorm;
     if (fw < sdv[4 * code + 3]) {  // r < 1 / lead: the reference's exp comparison decides
       const double sd = sdv[4 * code];
-      if (fw < exp(-(L.c_frac * L.c_frac) / (2.0 * sd * sd)) / sdv[4 * code + 2]) {
+      if (fw < RG_COS_EXP(-(L.c_frac * L.c_frac) / (2.0 * sd * sd)) / sdv[4 * code + 2]) {
         en[L.oi] = (long long)L.c_int;
         done = true;
       }
@@ -2224,14 +2232,14 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
   } else if (st == kCoWedge) {  // gaussian_rounded.go:109-113
     const int zi = (L.st >> 8) & 127;
     const double f0 = Zg.fn[zi - 1], f1 = Zg.fn[zi];
-    if (fw * (f0 - f1) < exp(-0.5 * L.t * L.t) - f1) {
+    if (fw * (f0 - f1) < RG_COS_EXP(-0.5 * L.t * L.t) - f1) {
       nf = L.t;
       have_nf = true;
     } else {
       nst = kCoNorm;
     }
   } else {  // kCoTailU / kCoTailV, gaussian_rounded.go:94-101
-    const double lg = -log(fw);
+    const double lg = -RG_COS_LOG(fw);
     if (st == kCoTailU) {
       L.t = lg * (1.0 / rn);
       nst = kCoTailV;
