@@ -39,6 +39,7 @@
 #include "csprng_host.hpp"
 #include "field.hpp"
 #include "host_field.hpp"
+#include "mac_mfma.hpp"
 #include "ntt64.hpp"
 
 namespace rg {
@@ -2759,6 +2760,8 @@ struct rg_jindo {
   rg::DevBuf ck_in, ck_mlwe, ck_out;  // the commit key, device-resident (entities.go:21-73 layouts)
   rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3_kernel (inner, outer)
   bool mac3_q = false, mac3_o = false;
+  rg::DevBuf ckm_in, ckm_out;  // the same as base-256 digits for mac_mfma (inner, outer)
+  int mfma_q = 0, mfma_o = 0;  // digits per residue of the MFMA MAC (0: mac3h / mac_kernel)
   uint64_t base_inv;
   std::mutex mu;  // guards `scratch` and `aux`
   std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
@@ -3066,6 +3069,34 @@ static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
   return a;
 }
 
+static MfmaPrime mfma_prime(const RnsPrime& P) { return MfmaPrime{P.q, P.rinv, P.rinv_sh, P.one_sh}; }
+
+// MacArgs (legacy kernel layout) -> MfmaMacArgs over the digit key `key` (mac_mfma_key_dev)
+static MfmaMacArgs mfma_args(const MacArgs& m, const DevBuf& key) {
+  MfmaMacArgs a;
+  memset(&a, 0, sizeof(a));
+  a.per_col = (long long)m.nl * m.d;
+  a.ncols = m.ncols;
+  a.J = m.J;
+  a.T1 = m.T1;
+  a.T2 = m.T2;
+  a.Tc = (m.T1 + m.T2 + 7) / 8;
+  mac_mfma_key_ptrs(key, a.per_col, m.T1 + m.T2, &a.Ak, &a.corr);
+  a.B1 = m.B1;
+  a.b1_col = m.b1_col;
+  a.b1_term = m.b1_term;
+  a.B2 = m.B2;
+  a.b2_col = m.b2_col;
+  a.b2_term = m.b2_term;
+  a.C = m.C;
+  a.c_col = m.c_col;
+  a.c_j = m.c_j;
+  a.out = m.out;
+  a.d = m.d;
+  for (int l = 0; l < m.nl && l < kMfmaMaxQ; ++l) a.P[l] = mfma_prime(m.P[l]);
+  return a;
+}
+
 // A handle's buffers belong to the device it was created on
 static rg_status on_device(const rg_jindo* J) {
   int cur = -1;
@@ -3106,7 +3137,9 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   ma.c_j = (long long)nq * d;
   ma.out = sc->com.as<uint64_t>();
   for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
-  if (J->mac3_q) {
+  if (J->mfma_q) {
+    RG_TRY(launch_mac_mfma(mfma_args(ma, J->ckm_in), J->mfma_q, st));
+  } else if (J->mac3_q) {
     RG_TRY(launch_mac3(mac3_args(ma, J->ck3_in.as<uint64_t>(), mac3_fold_period(J->rq, nq)), st));
   } else {
     RG_TRY(launch_mac(ma, st));
@@ -3143,7 +3176,9 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   mo.b1_term = (long long)nqo * d;
   mo.out = sc->ocom.as<uint64_t>();
   for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
-  if (J->mac3_o) {
+  if (J->mfma_o) {
+    RG_TRY(launch_mac_mfma(mfma_args(mo, J->ckm_out), J->mfma_o, st));
+  } else if (J->mac3_o) {
     RG_TRY(launch_mac3(mac3_args(mo, J->ck3_out.as<uint64_t>(), mac3_fold_period(J->ro, nqo)), st));
   } else {
     RG_TRY(launch_mac(mo, st));
@@ -3798,6 +3833,22 @@ static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
   const size_t pcq = (size_t)p.nq * p.d, pco = (size_t)p.nqo * p.d;
   J->mac3_q = !legacy && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
   J->mac3_o = !legacy && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
+  // RINGO_JINDO_MAC: l = mac_kernel, h = mac3h (VALU), default = the MFMA MAC where it applies
+  const bool no_mfma = legacy || (getenv("RINGO_JINDO_MAC") && getenv("RINGO_JINDO_MAC")[0] == 'h');
+  {
+    uint64_t pq[kMaxQ], po[kMaxQ];
+    MfmaPrime mq[kMaxQ], mo[kMaxQ];
+    for (int l = 0; l < p.nq; ++l) pq[l] = J->rq[l].q, mq[l] = mfma_prime(J->rq[l]);
+    for (int l = 0; l < p.nqo; ++l) po[l] = J->ro[l].q, mo[l] = mfma_prime(J->ro[l]);
+    J->mfma_q = no_mfma ? 0 : mac_mfma_nb(pq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
+    J->mfma_o = no_mfma ? 0 : mac_mfma_nb(po, p.nqo, p.out_msis, p.dcmp, p.d);
+    if (J->mfma_q)
+      RG_TRY(mac_mfma_key_dev(J->ck_in.as<uint64_t>(), p.rows, J->ck_mlwe.as<uint64_t>(), p.mlwe, p.in_msis,
+                              (long long)pcq, p.d, J->mfma_q, mq, p.nq, J->ckm_in, st));
+    if (J->mfma_o)
+      RG_TRY(mac_mfma_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, (long long)pco, p.d,
+                              J->mfma_o, mo, p.nqo, J->ckm_out, st));
+  }
   if (J->mac3_q)
     RG_TRY(mac3_key_dev(J->ck_in.as<uint64_t>(), p.rows, J->ck_mlwe.as<uint64_t>(), p.mlwe, p.in_msis, pcq, J->ck3_in, st));
   if (J->mac3_o) RG_TRY(mac3_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, pco, J->ck3_out, st));

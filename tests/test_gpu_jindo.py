@@ -233,3 +233,25 @@ def test_evaluate_batch_shards_sum_to_whole():
     for k in summed:
         assert torch.equal(summed[k], whole[k]), k
 
+
+
+@pytest.mark.parametrize("name,nv", [("t14_b1", 16384), ("mult_t8193_b12", 8193), ("t10_b8", 1024)])
+def test_mac_paths_agree(name, nv, monkeypatch):
+    """The three inner/outer MAC kernels (the MFMA digit MAC, mac3h on the VALU, mac_kernel)
+    produce the same Opening.InCommit and Commitment.Value bit for bit; RINGO_JINDO_MAC is read
+    when a prover's commit key is installed."""
+    P, q, params = _setup(name)
+    v = make_v(q, nv, seed=5)
+    rnd = make_randomness(P, q, seed=9)
+    outs = {}
+    for mode in ("", "h", "l"):
+        if mode:
+            monkeypatch.setenv("RINGO_JINDO_MAC", mode)
+        else:
+            monkeypatch.delenv("RINGO_JINDO_MAC", raising=False)
+        prv = jindo.NewProver(params, b"Jindo!")
+        com, op = prv.Commit(v, jindo.Randomness(**rnd))
+        outs[mode] = (op.InCommit.copy(), com.Value.copy())
+    for mode in ("h", "l"):
+        assert (outs[""][0] == outs[mode][0]).all(), (name, mode, "InCommit")
+        assert (outs[""][1] == outs[mode][1]).all(), (name, mode, "Commitment")
