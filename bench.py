@@ -342,7 +342,8 @@ def counters():
 
 
 # the kernels of one step of each line (setup kernels and the Evaluate MACs excluded)
-_DET = ("digits_kernel", "prep256_kernel", "mac3_kernel<", "mac3g_kernel<", "mac3h_kernel<", "round_kernel")
+_DET = ("digits_kernel", "prep256_kernel", "mac3_kernel<", "mac3g_kernel<", "mac3h_kernel<", "mac_mfma_kernel<",
+        "round_kernel")
 _SAMP = ("cdt_noise_kernel", "cdt_tail_kernel", "cosac_noise_kernel", "cdt2_noise_kernel", "cosac2_noise_kernel",
          "mlwe_noise_kernel", "uniform_elems_kernel")
 # l4: the 2^16 ntt256_pass launches only (the profiled run also executes the Buckler rank-2^15 ones)

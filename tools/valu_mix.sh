@@ -4,7 +4,7 @@
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
-for f in jindo ntt_l1_lazy ntt_l4_fast; do
+for f in jindo mac_mfma ntt_l1_lazy ntt_l4_fast; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Wno-unused-function -Wno-unused-result \
     -I"$R/include" --cuda-device-only -S -o "$T/$f.s" "$R/ringo-snark_amd/csrc/$f.hip" 2>/dev/null &
 done
