@@ -222,9 +222,12 @@ int mac_mfma_nb(const uint64_t* primes, int nl, int J, int T, int d) {
   const int NB = std::max(4, (bits + 2 + 7) / 8);  // q < 2^(8 NB - 2): the balanced top digit fits
   if (NB > 8) return 0;
   if ((double)((T + 7) / 8 * 8) * NB * 16384.0 >= 2147483648.0) return 0;  // int32 diagonal sums
-  // |sum_t A b'| < 2^126 (the fold's signed 128-bit value): T q max(q, bxor)
-  const double lq = bits, lx = std::log2((double)mac_mfma_bxor(NB) + 1.0);
-  if (std::log2((double)T) + lq + std::max(lq, lx) >= 125.0) return 0;
+  // |sum_t A b'| < T q max(q, bxor) must stay below 2^126, so that the fold's signed 128-bit
+  // value and its high word (int64) cannot overflow (configs[4]: 545 x 2^58 x 2^58 = 2^125.1)
+  double lq = 0;
+  for (int l = 0; l < nl; ++l) lq = std::max(lq, std::log2((double)primes[l]));
+  const double lx = std::log2((double)mac_mfma_bxor(NB) + 1.0);
+  if (std::log2((double)T) + lq + std::max(lq, lx) >= 126.0) return 0;
   return NB;
 }
 
