@@ -38,7 +38,16 @@ namespace rg {
 
 typedef int mfma_v4i __attribute__((ext_vector_type(4)));
 
-constexpr int kMfmaStages = 4;                  // LDS ring depth
+#ifndef RG_MFMA_STAGES
+#define RG_MFMA_STAGES 4
+#endif
+#ifndef RG_MFMA_PIPE
+#define RG_MFMA_PIPE 1  // chunk c + 1's LDS reads overlap chunk c's MFMAs (0: read, then compute)
+#endif
+#ifndef RG_MFMA_BLINE
+#define RG_MFMA_BLINE 0  // 1: each opening DMA covers 8 whole 128-B lines (LDS image [t][col half][lk pair][col 8])
+#endif
+constexpr int kMfmaStages = RG_MFMA_STAGES;     // LDS ring depth
 constexpr int kMfmaBWords = 8 * 8 * 16 * 2;     // opening words per stage: [t 8][lk pair 8][col 16][2]
 constexpr int kMfmaStageWords = kMfmaBWords * 2;  // + the 16 waves' key chunks [w][64 lanes][2]
 
@@ -72,7 +81,9 @@ __global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
   const int T = a.T1 + a.T2, Tc = a.Tc;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
   // this lane's opening chunk of every stage: term t = w >> 1, lk pair dp, column dcol
-  const int dcol = lane & 15, dp = ((w & 1) << 2) | (lane >> 4), dt = w >> 1;
+  // (BLINE: lane = lk pair x 8 + column within the half w & 1, so 8 lanes read one whole line)
+  const int dcol = RG_MFMA_BLINE ? ((w & 1) << 3) | (lane & 7) : lane & 15;
+  const int dp = RG_MFMA_BLINE ? lane >> 3 : ((w & 1) << 2) | (lane >> 4), dt = w >> 1;
   const long long dc = std::min<long long>(c0 + dcol, a.ncols - 1);
   // the wave's key chunk (1 KiB of [lk][chunk][64 lanes][2]): lane's own 16 B
   const uint64_t* akey = a.Ak + (lk0 + w) * Tc * 128 + 2 * lane;
@@ -94,19 +105,20 @@ __global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
   for (int k = 0; k < kMfmaStages - 1; ++k) stage(k);
   // LDS words of this lane's two opening values in a stage: term 2 (lane >> 4) + {0, 1}, its
   // lk = lk0 + w (pair w >> 1, half w & 1), column lane & 15
-  const int rd = ((2 * (lane >> 4) * 8 + (w >> 1)) * 16 + (lane & 15)) * 2 + (w & 1);
-  for (int c = 0; c < Tc; ++c) {
-    mfma_wait_vm<2 * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
-    __builtin_amdgcn_s_barrier();           // ... for every wave; stage c - 1 is free
-    stage(c + kMfmaStages - 1);
-    const uint64_t* st = ring + (c % kMfmaStages) * kMfmaStageWords;
+  const int rd = RG_MFMA_BLINE
+                     ? (((2 * (lane >> 4) * 2 + ((lane >> 3) & 1)) * 8 + (w >> 1)) * 8 + (lane & 7)) * 2 + (w & 1)
+                     : ((2 * (lane >> 4) * 8 + (w >> 1)) * 16 + (lane & 15)) * 2 + (w & 1);
+  // one chunk's operands from its LDS stage: the lane's two opening words (offset) and key words
+  auto rdstage = [&](int chunk, mfma_v4i& bv, ulonglong2& ak) {
+    const uint64_t* st = ring + (chunk % kMfmaStages) * kMfmaStageWords;
     const uint64_t b0 = st[rd] ^ a.bxor, b1 = st[rd + 256] ^ a.bxor;  // + 256 words: term + 1
-    const ulonglong2 ak = *reinterpret_cast<const ulonglong2*>(st + kMfmaBWords + w * 128 + 2 * lane);
-    mfma_v4i bv;
+    ak = *reinterpret_cast<const ulonglong2*>(st + kMfmaBWords + w * 128 + 2 * lane);
     bv[0] = (int)(uint32_t)b0;
     bv[1] = (int)(uint32_t)(b0 >> 32);
     bv[2] = (int)(uint32_t)b1;
     bv[3] = (int)(uint32_t)(b1 >> 32);
+  };
+  auto mfmas = [&](const mfma_v4i& bv, const ulonglong2& ak) {
 #pragma unroll
     for (int s = 0; s < ND; ++s) {
       const int sh = NB - 1 - s;  // A operand of diagonal s: byte b = digit s - b
@@ -119,7 +131,35 @@ __global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
       av[3] = (int)(uint32_t)(x1 >> 32);
       acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[s], 0, 0, 0);
     }
+  };
+#if RG_MFMA_PIPE
+  // chunk c + 1's operands are read from LDS while chunk c's MFMAs run: at the top of iteration
+  // c the stages 0 .. c + S - 2 are issued and c + 1 must have landed (S - 3 stages in flight)
+  mfma_v4i bcur, bnext;
+  ulonglong2 kcur, knext;
+  mfma_wait_vm<2 * (kMfmaStages - 2)>();
+  __builtin_amdgcn_s_barrier();
+  rdstage(0, bcur, kcur);
+  for (int c = 0; c < Tc; ++c) {
+    mfma_wait_vm<2 * (kMfmaStages - 3)>();
+    __builtin_amdgcn_s_barrier();  // stage c + 1 landed for every wave; stage c - 1 (read in c - 2) is free
+    stage(c + kMfmaStages - 1);
+    if (c + 1 < Tc) rdstage(c + 1, bnext, knext);
+    mfmas(bcur, kcur);
+    bcur = bnext;
+    kcur = knext;
   }
+#else
+  for (int c = 0; c < Tc; ++c) {
+    mfma_wait_vm<2 * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
+    __builtin_amdgcn_s_barrier();           // ... for every wave; stage c - 1 is free
+    stage(c + kMfmaStages - 1);
+    mfma_v4i bv;
+    ulonglong2 ak;
+    rdstage(c, bv, ak);
+    mfmas(bv, ak);
+  }
+#endif
   mfma_wait_vm<0>();
   __syncthreads();
   // fold: lane holds rows j = 4 (lane >> 4) + r of column lane & 15 for lk = lk0 + w
