@@ -41,15 +41,10 @@ typedef int mfma_v4i __attribute__((ext_vector_type(4)));
 #ifndef RG_MFMA_STAGES
 #define RG_MFMA_STAGES 4
 #endif
-#ifndef RG_MFMA_PIPE
-#define RG_MFMA_PIPE 1  // chunk c + 1's LDS reads overlap chunk c's MFMAs (0: read, then compute)
+#ifndef RG_MFMA_LK
+#define RG_MFMA_LK 16  // lk per workgroup: 16 (1024 threads, one 128-B line) or 8 (512 threads, 2 per CU: measured 30% slower)
 #endif
-#ifndef RG_MFMA_BLINE
-#define RG_MFMA_BLINE 0  // 1: each opening DMA covers 8 whole 128-B lines (LDS image [t][col half][lk pair][col 8])
-#endif
-constexpr int kMfmaStages = RG_MFMA_STAGES;     // LDS ring depth
-constexpr int kMfmaBWords = 8 * 8 * 16 * 2;     // opening words per stage: [t 8][lk pair 8][col 16][2]
-constexpr int kMfmaStageWords = kMfmaBWords * 2;  // + the 16 waves' key chunks [w][64 lanes][2]
+constexpr int kMfmaStages = RG_MFMA_STAGES;  // LDS ring depth
 
 __device__ __forceinline__ void mfma_glds16(const void* gsrc, uint32_t lds_dst) {
   uint32_t keep;
@@ -68,57 +63,61 @@ __device__ __forceinline__ void mfma_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int NB>
-__global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
-  constexpr int ND = 2 * NB - 1;  // diagonals
-  __shared__ uint64_t ring[kMfmaStages * kMfmaStageWords];
+// LK lk x 16 columns per workgroup, wave w = lk0 + w.  Stage image (u64 words): the opening
+// [t 8][lk pair LK/2][col 16][2] (LK KiB), then the waves' key chunks [w][64 lanes][2] (LK KiB).
+template <int NB, int LK>
+__global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs a) {
+  constexpr int ND = 2 * NB - 1;      // diagonals
+  constexpr int NP = LK / 2;          // lk pairs
+  constexpr int BW = 8 * NP * 16 * 2;  // opening words per stage
+  constexpr int SW = BW + LK * 128;    // stage words
+  static_assert(16 * 16 * LK <= kMfmaStages * SW, "output stage must fit the ring");
+  __shared__ uint64_t ring[kMfmaStages * SW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long nct = (a.ncols + 15) / 16;
   unsigned g = blockIdx.x;
   if ((gridDim.x & 7) == 0) g = (g & 7) * (gridDim.x >> 3) + (g >> 3);  // XCD-major
-  const long long lk0 = (long long)(g / nct) * 16, c0 = (long long)(g % nct) * 16;
+  const long long lk0 = (long long)(g / nct) * LK, c0 = (long long)(g % nct) * 16;
   const int T = a.T1 + a.T2, Tc = a.Tc;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-  // this lane's opening chunk of every stage: term t = w >> 1, lk pair dp, column dcol
-  // (BLINE: lane = lk pair x 8 + column within the half w & 1, so 8 lanes read one whole line)
-  const int dcol = RG_MFMA_BLINE ? ((w & 1) << 3) | (lane & 7) : lane & 15;
-  const int dp = RG_MFMA_BLINE ? lane >> 3 : ((w & 1) << 2) | (lane >> 4), dt = w >> 1;
+  // the lane's opening chunk of every stage: position w * 64 + lane of [t][lk pair][col]
+  constexpr int PW = NP * 16;  // chunks per term
+  const int dpos = w * 64 + lane, dt = dpos / PW, dp = (dpos % PW) >> 4, dcol = lane & 15;
   const long long dc = std::min<long long>(c0 + dcol, a.ncols - 1);
-  // the wave's key chunk (1 KiB of [lk][chunk][64 lanes][2]): lane's own 16 B
+  // the wave's key chunk (1 KiB of [lk][chunk][64 lanes][2]): the lane's own 16 B
   const uint64_t* akey = a.Ak + (lk0 + w) * Tc * 128 + 2 * lane;
-  // stage `chunk`: 2 LDS-DMAs per wave (opening 16 B, key 16 B per lane); past the last chunk they
-  // reload valid addresses into a free stage, so every iteration issues the same count
+  // stage `chunk`: 2 LDS-DMAs per wave (16 B of opening, 16 B of key per lane); past the last
+  // chunk they reload valid addresses into a free stage, so every iteration issues the same count
   auto stage = [&](int chunk) {
     int t = chunk * 8 + dt;
     if (t >= T) t = T - 1;  // the key's padded terms are zero
     const uint64_t* src = t < a.T1 ? a.B1 + dc * a.b1_col + (long long)t * a.b1_term
                                    : a.B2 + dc * a.b2_col + (long long)(t - a.T1) * a.b2_term;
-    const uint32_t base = ring_lds + (uint32_t)((chunk % kMfmaStages) * kMfmaStageWords) * 8u;
+    const uint32_t base = ring_lds + (uint32_t)((chunk % kMfmaStages) * SW) * 8u;
     mfma_glds16(src + lk0 + 2 * dp, base + (uint32_t)(w * 128) * 8u);
-    mfma_glds16(akey + (long long)std::min(chunk, Tc - 1) * 128, base + (uint32_t)(kMfmaBWords + w * 128) * 8u);
+    mfma_glds16(akey + (long long)std::min(chunk, Tc - 1) * 128, base + (uint32_t)(BW + w * 128) * 8u);
   };
   mfma_v4i acc[ND];
 #pragma unroll
   for (int s = 0; s < ND; ++s) acc[s] = mfma_v4i{0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < kMfmaStages - 1; ++k) stage(k);
-  // LDS words of this lane's two opening values in a stage: term 2 (lane >> 4) + {0, 1}, its
-  // lk = lk0 + w (pair w >> 1, half w & 1), column lane & 15
-  const int rd = RG_MFMA_BLINE
-                     ? (((2 * (lane >> 4) * 2 + ((lane >> 3) & 1)) * 8 + (w >> 1)) * 8 + (lane & 7)) * 2 + (w & 1)
-                     : ((2 * (lane >> 4) * 8 + (w >> 1)) * 16 + (lane & 15)) * 2 + (w & 1);
-  // one chunk's operands from its LDS stage: the lane's two opening words (offset) and key words
-  auto rdstage = [&](int chunk, mfma_v4i& bv, ulonglong2& ak) {
-    const uint64_t* st = ring + (chunk % kMfmaStages) * kMfmaStageWords;
-    const uint64_t b0 = st[rd] ^ a.bxor, b1 = st[rd + 256] ^ a.bxor;  // + 256 words: term + 1
-    ak = *reinterpret_cast<const ulonglong2*>(st + kMfmaBWords + w * 128 + 2 * lane);
+  // LDS words of the lane's two opening values: terms 2 (lane >> 4) + {0, 1}, lk = lk0 + w
+  // (pair w >> 1, half w & 1), column lane & 15
+  const int rd = ((2 * (lane >> 4) * NP + (w >> 1)) * 16 + (lane & 15)) * 2 + (w & 1);
+  for (int c = 0; c < Tc; ++c) {
+    mfma_wait_vm<2 * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
+    __builtin_amdgcn_s_barrier();           // ... for every wave; stage c - 1 is free
+    stage(c + kMfmaStages - 1);
+    const uint64_t* st = ring + (c % kMfmaStages) * SW;
+    const uint64_t b0 = st[rd] ^ a.bxor, b1 = st[rd + NP * 32] ^ a.bxor;  // + NP 32 words: term + 1
+    const ulonglong2 ak = *reinterpret_cast<const ulonglong2*>(st + BW + w * 128 + 2 * lane);
+    mfma_v4i bv;
     bv[0] = (int)(uint32_t)b0;
     bv[1] = (int)(uint32_t)(b0 >> 32);
     bv[2] = (int)(uint32_t)b1;
     bv[3] = (int)(uint32_t)(b1 >> 32);
-  };
-  auto mfmas = [&](const mfma_v4i& bv, const ulonglong2& ak) {
 #pragma unroll
     for (int s = 0; s < ND; ++s) {
       const int sh = NB - 1 - s;  // A operand of diagonal s: byte b = digit s - b
@@ -131,38 +130,10 @@ __global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
       av[3] = (int)(uint32_t)(x1 >> 32);
       acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[s], 0, 0, 0);
     }
-  };
-#if RG_MFMA_PIPE
-  // chunk c + 1's operands are read from LDS while chunk c's MFMAs run: at the top of iteration
-  // c the stages 0 .. c + S - 2 are issued and c + 1 must have landed (S - 3 stages in flight)
-  mfma_v4i bcur, bnext;
-  ulonglong2 kcur, knext;
-  mfma_wait_vm<2 * (kMfmaStages - 2)>();
-  __builtin_amdgcn_s_barrier();
-  rdstage(0, bcur, kcur);
-  for (int c = 0; c < Tc; ++c) {
-    mfma_wait_vm<2 * (kMfmaStages - 3)>();
-    __builtin_amdgcn_s_barrier();  // stage c + 1 landed for every wave; stage c - 1 (read in c - 2) is free
-    stage(c + kMfmaStages - 1);
-    if (c + 1 < Tc) rdstage(c + 1, bnext, knext);
-    mfmas(bcur, kcur);
-    bcur = bnext;
-    kcur = knext;
   }
-#else
-  for (int c = 0; c < Tc; ++c) {
-    mfma_wait_vm<2 * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
-    __builtin_amdgcn_s_barrier();           // ... for every wave; stage c - 1 is free
-    stage(c + kMfmaStages - 1);
-    mfma_v4i bv;
-    ulonglong2 ak;
-    rdstage(c, bv, ak);
-    mfmas(bv, ak);
-  }
-#endif
   mfma_wait_vm<0>();
   __syncthreads();
-  // fold: lane holds rows j = 4 (lane >> 4) + r of column lane & 15 for lk = lk0 + w
+  // fold: the lane holds rows j = 4 (lane >> 4) + r of column lane & 15 for lk = lk0 + w
   const long long lk = lk0 + w;
   const MfmaPrime& P = a.P[(int)(lk0 / a.d)];
   const uint64_t q = P.q;
@@ -181,15 +152,15 @@ __global__ __launch_bounds__(1024, 1) void mac_mfma_kernel(MfmaMacArgs a) {
       res = mod_sub(res, shoup_mul((uint64_t)(-(hi + 1)) + 1, 1, P.one_sh, q), q);
     }
     res = mod_add(res, a.corr[lk * 16 + j], q);
-    ring[((lane & 15) * 16 + j) * 16 + w] = res;  // [col][j][lk]
+    ring[((lane & 15) * 16 + j) * LK + w] = res;  // [col][j][lk]
   }
   __syncthreads();
-  // 256 rows (col, j) of 16 lk = 128 B: 8 threads x 16 B per row
-  for (int i = tid; i < 256 * 8; i += 1024) {
-    const int row = i >> 3, part = i & 7, cl = row >> 4, j = row & 15;
+  // 256 rows (col, j) of LK lk (LK * 8 B): LK / 2 threads x 16 B per row
+  for (int i = tid; i < 256 * NP; i += 64 * LK) {
+    const int row = i / NP, part = i % NP, cl = row >> 4, j = row & 15;
     const long long col = c0 + cl;
     if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r0 = ring[row * 16 + 2 * part], r1 = ring[row * 16 + 2 * part + 1];
+    uint64_t r0 = ring[row * LK + 2 * part], r1 = ring[row * LK + 2 * part + 1];
     const long long l = lk0 + 2 * part;
     if (a.C) {
       const ulonglong2 cv = *reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + l);
@@ -306,14 +277,15 @@ rg_status launch_mac_mfma(const MfmaMacArgs& args, int NB, hipStream_t st) {
     set_last_error("mac_mfma: shape outside the kernel's assumptions");
     return RG_ERR_INVALID;
   }
-  const long long blocks = (a.per_col / 16) * ((a.ncols + 15) / 16);
-  const dim3 g((unsigned)blocks), b(1024);
+  constexpr int LK = RG_MFMA_LK;
+  const long long blocks = (a.per_col / LK) * ((a.ncols + 15) / 16);
+  const dim3 g((unsigned)blocks), b(64 * LK);
   switch (NB) {
-    case 4: hipLaunchKernelGGL(mac_mfma_kernel<4>, g, b, 0, st, a); break;
-    case 5: hipLaunchKernelGGL(mac_mfma_kernel<5>, g, b, 0, st, a); break;
-    case 6: hipLaunchKernelGGL(mac_mfma_kernel<6>, g, b, 0, st, a); break;
-    case 7: hipLaunchKernelGGL(mac_mfma_kernel<7>, g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL(mac_mfma_kernel<8>, g, b, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((mac_mfma_kernel<4, LK>), g, b, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((mac_mfma_kernel<5, LK>), g, b, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((mac_mfma_kernel<6, LK>), g, b, 0, st, a); break;
+    case 7: hipLaunchKernelGGL((mac_mfma_kernel<7, LK>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((mac_mfma_kernel<8, LK>), g, b, 0, st, a); break;
   }
   return check_launch("jindo mac_mfma");
 }
