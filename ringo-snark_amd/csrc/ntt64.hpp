@@ -242,6 +242,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_buf(const void* p) {
 #ifndef RG_NTT_LTW
 #define RG_NTT_LTW 1  // L-round twiddles staged in LDS per tile (COL, RP); 0 = per-lane global loads
 #endif
+#ifndef RG_NTT_PRIO
+#define RG_NTT_PRIO 0  // A/B knob: 1 = tile loads issued at s_setprio 3 (6% slower), 2 = butterflies at s_setprio 2
+#endif
 #ifndef RG_NTT_SAUX
 #define RG_NTT_SAUX RG_NTT_AUX
 #endif
@@ -380,7 +383,8 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     if (tid < 384u)
       reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
   }
-  // ---- global load
+  // ---- global load (RG_NTT_PRIO: the wave issues its tile loads at raised priority)
+  if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(3);
   if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = (uint64_t)(tid * 0x9E3779B9u + tile * 8u + (uint32_t)y);
@@ -399,6 +403,8 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
   }
+  if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+  if constexpr (RG_NTT_PRIO == 2) __builtin_amdgcn_s_setprio(2);  // 2: butterflies at raised priority
   // PROBE & 4: the result stays live through a store that never fires (values are < 2q < 2^64 - 1)
   auto st64 = [&](uint64_t x, uint32_t voff, uint32_t soff) {
     if constexpr ((PROBE & 4) != 0) {
