@@ -173,27 +173,51 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     ok = bool(torch.equal(x, ref))  # fwd then inv is the identity: full-size self-check
     kern_ms = ev.total_ms()
     floor_ms = None
-    if L == 1:
-        # the compute floor of the same launches: rg_set_probe(4) swaps in the ntt16_pass variant
-        # with no HBM data loads / stores (butterflies, twiddle loads and LDS exchanges as in the
-        # production kernel), timed the same way; x is not written while the probe is set
-        lib = ringo.lib()
-        if hasattr(lib, "rg_set_probe") and lib.rg_set_probe(4) == 0:
-            try:
-                for _ in range(max(2, warmup)):
-                    step()
-                torch.cuda.synchronize()
-                evp = Events(torch, stream)
-                evp.start()
-                for _ in range(steps):
-                    step()
-                evp.stop()
-                torch.cuda.synchronize()
-                floor_ms = evp.total_ms() / steps
-            finally:
-                lib.rg_set_probe(0)
-            ok = ok and bool(torch.equal(x, ref))
+    if logn == 16:
+        floor_ms = compute_floor(torch, ringo, q, L, N, batch, x, stream, steps, warmup)
+        ok = ok and bool(torch.equal(x, ref))
     return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L, compute_floor_ms=floor_ms)
+
+
+def compute_floor(torch, ringo, q, L, N, batch, x, stream, steps, warmup):
+    """The compute floor of the step's own launches: the experiments build (libringo_exp.so, a
+    second copy of the library loaded beside the product) with rg_set_probe(4) (L = 1: ntt16_pass)
+    or (5) (L = 4: ntt256_pass) runs the same kernels with their HBM data loads and stores removed
+    (butterflies, twiddle loads and LDS exchanges kept), timed the same way.  x is not written.
+    The product library refuses the probe (include/ringo.h), so this is the only way to it."""
+    import ctypes
+    from ringo import _lib
+    try:
+        E = _lib.load(_lib.EXP_LIB_PATH)
+    except RuntimeError:
+        return None
+    probe = 4 if L == 1 else 5
+    ql = (ctypes.c_uint64 * L)(*[(q >> (64 * i)) & ((1 << 64) - 1) for i in range(L)])
+    f, h = ctypes.c_void_p(), ctypes.c_void_p()
+    if E.rg_field_create(L, ql, ctypes.byref(f)) != 0 or E.rg_ntt_create(f, N, 1, ctypes.byref(h)) != 0:
+        return None
+    p, s = ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(stream.cuda_stream)
+
+    def pstep():
+        assert E.rg_ntt_fwd_dev(h, p, p, batch, s) == 0 and E.rg_ntt_inv_dev(h, p, p, batch, s) == 0
+
+    try:
+        if E.rg_set_probe(probe) != 0:
+            return None
+        for _ in range(max(2, warmup)):
+            pstep()
+        torch.cuda.synchronize()
+        evp = Events(torch, stream)
+        evp.start()
+        for _ in range(steps):
+            pstep()
+        evp.stop()
+        torch.cuda.synchronize()
+        return evp.total_ms() / steps
+    finally:
+        E.rg_set_probe(0)
+        E.rg_ntt_destroy(h)
+        E.rg_field_destroy(f)
 
 
 def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world, eval_steps=0):
@@ -347,7 +371,7 @@ _DET = ("digits_kernel", "prep256_kernel", "mac3_kernel<", "mac3g_kernel<", "mac
 _SAMP = ("cdt_noise_kernel", "cdt_tail_kernel", "cosac_noise_kernel", "cdt2_noise_kernel", "cosac2_noise_kernel",
          "mlwe_noise_kernel", "uniform_elems_kernel")
 # l4: the 2^16 ntt256_pass launches only (the profiled run also executes the Buckler rank-2^15 ones)
-LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("16>(rg::Ntt256Args)",), "j14": _DET + _SAMP, "j16": _DET + _SAMP}
+LINE_KERNELS = {"ntt": ("ntt16_pass",), "l4": ("16, 0>(rg::Ntt256Args)",), "j14": _DET + _SAMP, "j16": _DET + _SAMP}
 
 
 _PROBE_KERNEL = re.compile(r"ntt16_pass<.*, [1-9][0-9]*>\(")  # PROBE != 0: rg_set_probe's measurement variants
@@ -677,9 +701,10 @@ def main():
             vb = dict(vb or {})
             vb.update({"compute_floor_ms_per_step": cf, "compute_frac": cf / (kern_ms / args.steps),
                        "compute_floor_note": "the same ntt16_pass launches with their HBM data loads and stores "
-                                             "removed (rg_set_probe(4): butterflies, twiddle loads, LDS exchanges "
-                                             "kept), HIP-event timed on the launch stream; compute_frac = that "
-                                             "time / the production step's kernel time"})
+                                             "removed (experiments build libringo_exp.so, rg_set_probe(4): "
+                                             "butterflies, twiddle loads, LDS exchanges kept), HIP-event timed on "
+                                             "the launch stream; compute_frac = that time / the production step's "
+                                             "kernel time"})
         out.update({
             "metric": "NTTs/sec (fwd+inv negacyclic, degree 2^16, 63-bit prime, batch 1024/GPU)",
             "value": world * 2 * args.batch / (ms_step / 1000.0),
@@ -713,6 +738,13 @@ def main():
         ms4, k4 = reduce_max(torch, dist, r4["wall_s"] * 1000.0 / st4, r4["kernel_ms"])
         vm = vec_mul_bench(torch, ringo, Q255, 4, 64 * N, 10, 11 + rank)
         tr4, vb4 = line_counters(C, "l4", 128, k4 / st4)
+        cf4 = r4.get("compute_floor_ms")
+        if cf4 is not None:
+            cf4 = reduce_max(torch, dist, cf4)
+            vb4 = dict(vb4 or {})
+            vb4.update({"compute_floor_ms_per_step": cf4, "compute_frac": cf4 / (k4 / st4),
+                        "compute_floor_note": "the same ntt256_pass launches without HBM data movement "
+                                              "(libringo_exp.so, rg_set_probe(5)), HIP-event timed"})
         out["l4_ntt"] = {"value": world * 2 * 64 / (ms4 / 1000.0), "unit": "NTT/s",
                          "config": "configs[3]: fwd+inv negacyclic NTT, N=2^16, 255-bit Jindo prime, batch 64/GPU",
                          "kernel": "ntt256_pass (4-limb Montgomery, q = 1 mod 2^64; VALU-bound)",

@@ -249,7 +249,11 @@ rg_status rg_jindo_commit_dev(const rg_jindo* j, size_t batch, const uint64_t* d
  * [cols+1][in_msis+mlwe][nq][d] (as Go holds them after commitColTo's encode and MLWE loops),
  * the inner Ajtai MACs, CRT rounding into Opening.InCommit [dcmp][nqo][d] (:144-176) and
  * outerCommitTo into Commitment.Value [out_msis][nq][d] (:180-202).  `_dev`: `batch` openings
- * back to back, asynchronous on `stream`. */
+ * back to back, asynchronous on `stream`.
+ * Precondition (as in Lattigo, whose ring elements are always reduced): every word of `enc`,
+ * `mlwe` and of the commit key given to rg_jindo_create* is a canonical residue (< its prime).
+ * The MFMA MAC splits words into base-256 digits under that bound; a non-canonical word gives a
+ * wrong commitment, not an error. */
 rg_status rg_jindo_commit_core(const rg_jindo* j, const uint64_t* enc, const uint64_t* mlwe, uint64_t* o_incom,
                                uint64_t* o_com);
 rg_status rg_jindo_commit_core_dev(const rg_jindo* j, size_t batch, const uint64_t* d_enc, const uint64_t* d_mlwe,
@@ -263,6 +267,12 @@ size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
  * (a destroyed stream's handle value may be reused by a new stream).  Not concurrent with calls
  * on that stream. */
 rg_status rg_jindo_release_stream(rg_jindo* j, void* stream);
+/* Which kernel runs the inner (prover.go:149-157) and outer (:180-191) Ajtai products of this
+ * handle: RG_MAC_MFMA (mac_mfma.hip, the matrix cores; needs canonical inputs, see
+ * rg_jindo_commit_core_dev), RG_MAC_VALU3 (mac3h), RG_MAC_GENERIC (mac_kernel).  Introspection
+ * only; no reference counterpart. */
+enum { RG_MAC_GENERIC = 0, RG_MAC_VALU3 = 1, RG_MAC_MFMA = 2 };
+rg_status rg_jindo_mac_kinds(const rg_jindo* j, int* inner, int* outer);
 
 /* ---- the prover's randomness on the device --------------------- */
 /* The standard deviations jindo.Parameters holds (params.go:99-111): ecdStdDev,
@@ -392,10 +402,12 @@ rg_status rg_memcpy_d2h(void* dst, const void* d_src, size_t bytes, void* stream
 rg_status rg_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes, void* stream);
 rg_status rg_stream_sync(void* stream);
 rg_status rg_set_device(int device);
-/* Measurement hook (bench.py's roofline block; not for production calls): probe 4 makes the
- * single-word 2^16 NTT launches (ntt16_pass) skip their HBM data loads and stores, so the same
- * launches time the kernel's compute floor (butterflies, twiddle loads, LDS exchanges); their
- * outputs are then meaningless.  0 restores the production kernels.  Process-wide. */
+/* Measurement hook.  libringo.so refuses every probe but 0 (RG_ERR_INVALID): no production call
+ * can switch a kernel.  Only the experiments build (libringo_exp.so, bench.py's compute-floor
+ * legs and tools/) honours it: probe 4 makes the single-word 2^16 NTT launches (ntt16_pass), probe
+ * 5 the q255 2^16 launches (ntt256_pass), skip their HBM data loads and stores, so the same
+ * launches time the kernel's compute floor; their outputs are then meaningless.  0 restores the
+ * production kernels.  Per calling thread. */
 rg_status rg_set_probe(int probe);
 /* the calling thread's current device (one rank per GPU: LOCAL_RANK -> rg_set_device) */
 rg_status rg_get_device(int* device);

@@ -1,6 +1,5 @@
 // capi.hip -- C-ABI entry points that are not kernel-specific: status strings, field
 // handles, device memory helpers.
-#include <atomic>
 #include <string>
 
 #include "common.hpp"
@@ -9,8 +8,6 @@
 namespace rg {
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& msg) { g_last_error = msg; }
-std::atomic<int> g_probe{0};
-int measure_probe() { return g_probe.load(std::memory_order_relaxed); }
 }  // namespace rg
 
 using namespace rg;
@@ -88,12 +85,6 @@ rg_status rg_stream_sync(void* stream) {
 }
 rg_status rg_set_device(int device) {
   RG_HIP(hipSetDevice(device));
-  return RG_OK;
-}
-
-rg_status rg_set_probe(int probe) {
-  if (probe != 0 && probe != 4) return RG_ERR_INVALID;
-  ::rg::g_probe.store(probe);
   return RG_OK;
 }
 

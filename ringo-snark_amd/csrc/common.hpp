@@ -13,7 +13,25 @@
 namespace rg {
 
 void set_last_error(const std::string& msg);
-// rg_set_probe: process-wide measurement probe (0 = production kernels)
+
+// Measurement / A-B switches.  libringo.so links knobs.hip, where every knob is unset (nullptr:
+// the production choice) and the probe is 0.  Only the experiments build, libringo_exp.so
+// (tools/experiments/knobs_env.hip), reads them from the RINGO_* environment and honours
+// rg_set_probe; the production library has no environment access at all.
+enum class Knob : int {
+  NttKernel,   // RINGO_NTT_KERNEL   r2 | r8 | r*: generic single-word / q255 pass kernels
+  NttChunkMb,  // RINGO_NTT_CHUNK_MB polys per pass pair bounded to this many MiB
+  NttPrefetch, // RINGO_NTT_PREFETCH 0: no next-tile register prefetch in ntt_r2
+  NttWgPerCu,  // RINGO_NTT_WG_PER_CU persistent ntt_r8 grid size
+  NttR8Pf,     // RINGO_NTT_R8_PF    1: persistent prefetching ntt_r8
+  JindoPrep,   // RINGO_JINDO_PREP   l: workgroup-per-polynomial prep_kernel
+  JindoPrepW,  // RINGO_JINDO_PREP_W minimum waves/SIMD of prep256 (1, 6, 8)
+  JindoMac,    // RINGO_JINDO_MAC    h: mac3h, l: mac_kernel instead of the MFMA MAC
+  JindoSplit,  // RINGO_JINDO_SPLIT  0: commit_sampled on the caller's stream only
+  Count
+};
+const char* knob(Knob k);
+// rg_set_probe's value on the calling thread (always 0 in libringo.so)
 int measure_probe();
 
 #define RG_HIP(call)                                                                            \

@@ -12,11 +12,12 @@
 //                      MForm(noise), X^slots negacyclic shift, - b*s, + MForm(digits)) or the
 //                      MLWE finalize (prover.go:130-141), then the 256-point negacyclic NTT per
 //                      RNS limb in registers (Lattigo ordering/roots).
-//   3. mac3_kernel     per-(limb, coeff) modular GEMM for the inner Ajtai product
+//   3. the inner Ajtai product, a per-(limb, coeff) modular GEMM
 //                      sum_k In[j][k]*Enc[k] + sum_k CK.MLWE[j][k]*MLWE[k] + MLWE[mlwe+j]
 //                      (prover.go:149-157): exact sums reduced once (MulCoeffsMontgomeryThenAdd
-//                      summed == (sum a*b) * 2^-64 mod q); mac_kernel is the fallback for
-//                      primes >= 2^60 or J > 16.
+//                      summed == (sum a*b) * 2^-64 mod q).  mac_mfma_kernel (mac_mfma.hip, the
+//                      matrix cores) where its digit bound holds; else mac3h_kernel (VALU);
+//                      mac_kernel for primes >= 2^60 or J > 16.
 //   4. round_kernel    workgroup per polynomial: IMForm, INTT, centred CRT (Garner, up to 4
 //                      primes), floor shift by the cut, Euclidean mod q', MForm, NTT in the
 //                      destination ring (prover.go:164-176, rns.go:76-114).
@@ -716,7 +717,7 @@ struct Mac3Args {
   int J, T1, T2, fold;  // fold: a multiple of kMac3Tc
   int Tp;               // T1 + T2 rounded up to kMac3Tc (the key's zero-padded term count)
   const uint64_t* As;   // [per_col][Tp][JP]
-  const uint32_t* Ss;   // [per_col][Tp][JP]  a0 + a1 of the same key words (mac3g's Karatsuba middle)
+  const uint32_t* Ss;   // [per_col][Tp][JP]  a0 + a1 of the same key words (the Karatsuba middle)
   const uint64_t* B1;
   long long b1_col, b1_term;
   const uint64_t* B2;
@@ -739,161 +740,20 @@ __device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
   a.s00 = a.s01 = a.s11 = 0;
 }
 
-// Karatsuba accumulators of mac3g: sm = sum (a0 + a1)(b0 + b1), so the middle sum is
+// Karatsuba accumulators: sm = sum (a0 + a1)(b0 + b1), so the middle sum is
 // s01 = sm - s00 - s11 (exact: sm holds every product of the four); folded like Mac3Acc
 __device__ __forceinline__ void mac3k_fold(Mac3Acc& a) {
   a.s01 -= a.s00 + a.s11;
   mac3_fold(a);
 }
 
-// JS = 2 would split the JP outputs of a (column, lk) across two waves (JP / 2 accumulators each,
-// 64 columns x 4 lk per workgroup, two workgroups per CU); measured slower at J = 10 and 16
-// (DESIGN.md §5), so only JS = 1 is instantiated.
-template <int JP, int JS>
-__global__ __launch_bounds__(512, JS == 2 ? 4 : 1) void mac3_kernel(Mac3Args a) {
-  constexpr int NLK = 8 / JS, JW = JP / JS;  // lk per workgroup, accumulators per lane
-  static_assert(JP * NLK * 64 <= 2 * kMac3Tc * NLK * 64, "output stage must fit the tile buffers");
-  static_assert(JW % 2 == 0 && NLK % 2 == 0, "16-B staging");
-  __shared__ uint64_t lds[2 * kMac3Tc * NLK * 64];  // two B tiles [tt][lk][col]; then the output stage
-  __shared__ uint64_t lda[2][NLK][kMac3Tc * JP];    // two key tiles [lk][tt][j]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lkw = w % NLK, jh = w / NLK;  // this wave's lk and output half
-  const long long nlkg = a.per_col / NLK;
-  const long long lk0 = (blockIdx.x % nlkg) * NLK, c0 = (blockIdx.x / nlkg) * 64;
-  const int lk = (int)lk0 + lkw;
-  const int T = a.T1 + a.T2;
-  // loader role: column c0 + lane, term tb + w, NLK consecutive lk (8 NLK bytes)
-  const long long lcol = c0 + lane;
-  const bool lval = lcol < a.ncols;
-  auto gload = [&](int tb, ulonglong2 (&v)[NLK / 2]) {
-    const int t = tb + w;
-    if (lval && t < T) {
-      const uint64_t* p = t < a.T1 ? a.B1 + lcol * a.b1_col + (long long)t * a.b1_term + lk0
-                                   : a.B2 + lcol * a.b2_col + (long long)(t - a.T1) * a.b2_term + lk0;
-      const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
-#pragma unroll
-      for (int i = 0; i < NLK / 2; ++i) v[i] = q[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < NLK / 2; ++i) v[i] = make_ulonglong2(0, 0);
-    }
-  };
-  auto lstore = [&](int buf, const ulonglong2 (&v)[NLK / 2]) {
-    uint64_t* L = lds + buf * (kMac3Tc * NLK * 64) + (w * NLK) * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < NLK / 2; ++i) {
-      L[(2 * i) * 64] = v[i].x;
-      L[(2 * i + 1) * 64] = v[i].y;
-    }
-  };
-  // key loader role: wave (lkw, jh) stages its own half of lk's slice (8 terms x JW words)
-  const ulonglong2* Aw = reinterpret_cast<const ulonglong2*>(a.As + (long long)lk * a.Tp * JP);
-  auto aload = [&](int tb, ulonglong2& v) {
-    const int tt = lane / (JW / 2), jj = lane % (JW / 2);
-    v = (lane < 4 * JW && tb + tt < T) ? Aw[((long long)(tb + tt) * JP + jh * JW) / 2 + jj] : make_ulonglong2(0, 0);
-  };
-  auto astore = [&](int buf, const ulonglong2& v) {
-    const int tt = lane / (JW / 2), jj = lane % (JW / 2);
-    if (lane < 4 * JW) reinterpret_cast<ulonglong2*>(lda[buf][lkw])[(tt * JP + jh * JW) / 2 + jj] = v;
-  };
-  Mac3Acc acc[JW];
-#pragma unroll
-  for (int j = 0; j < JW; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
-  ulonglong2 pre[NLK / 2], apre;
-  gload(0, pre);
-  aload(0, apre);
-  lstore(0, pre);
-  astore(0, apre);
-  __syncthreads();
-  int buf = 0, since = 0;
-  for (int tb = 0; tb < T; tb += kMac3Tc) {
-    const bool more = tb + kMac3Tc < T;
-    if (more) {
-      gload(tb + kMac3Tc, pre);
-      aload(tb + kMac3Tc, apre);
-    }
-    const uint64_t* L = lds + buf * (kMac3Tc * NLK * 64) + lkw * 64 + lane;
-    const uint64_t* LA = lda[buf][lkw] + jh * JW;
-#pragma unroll
-    for (int tt = 0; tt < kMac3Tc; ++tt) {
-      // terms past T were staged as zeros (B and key), so they add nothing
-      const uint64_t b = L[tt * NLK * 64];
-      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29);
-#pragma unroll
-      for (int j = 0; j < JW; ++j) {
-        const uint64_t av = LA[tt * JP + j];
-        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32);
-        Mac3Acc& z = acc[j];
-        z.s00 = mad64(a0, b0, z.s00);
-        z.s01 = mad64(a0, b1, z.s01);
-        // opaque to reassociation: without it the two middle products are summed first
-        // (mad with 0, mad, 64-bit add = 3 VALU instead of 2 v_mad_u64_u32 into s01)
-        asm("" : "+v"(z.s01));
-        z.s01 = mad64(a1, b0, z.s01);
-        z.s11 = mad64(a1, b1, z.s11);
-      }
-    }
-    since += kMac3Tc;
-    if (since >= a.fold) {
-#pragma unroll
-      for (int j = 0; j < JW; ++j) mac3_fold(acc[j]);
-      since = 0;
-    }
-    if (more) {
-      lstore(buf ^ 1, pre);
-      astore(buf ^ 1, apre);
-    }
-    __syncthreads();
-    buf ^= 1;
-  }
-  // reduce: (lo + hi 2^64) 2^-64 mod q = lo 2^-64 + hi (MulCoeffsMontgomeryThenAdd summed)
-  const RnsPrime& P = a.P[lk / a.d];
-  const uint64_t q = P.q;
-#pragma unroll
-  for (int j = 0; j < JW; ++j) {
-    mac3_fold(acc[j]);
-    uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
-    r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
-    lds[((jh * JW + j) * NLK + lkw) * 64 + lane] = r;  // [j][lk][col]
-  }
-  __syncthreads();
-  // store: (col, j) pairs, NLK consecutive lk = one 8 NLK-byte row each
-  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // NLK lk never straddle a limb (d % 8 == 0)
-  for (int pidx = tid; pidx < JP * 64; pidx += 512) {
-    const int c = pidx & 63, j = pidx >> 6;
-    const long long col = c0 + c;
-    if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r[NLK];
-#pragma unroll
-    for (int x = 0; x < NLK; ++x) r[x] = lds[(j * NLK + x) * 64 + c];
-    if (a.C) {
-      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
-#pragma unroll
-      for (int i = 0; i < NLK / 2; ++i) {
-        const ulonglong2 cv = cp[i];
-        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
-        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
-      }
-    }
-    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
-#pragma unroll
-    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
-  }
-}
-
-// ---- mac3g: the same products, tiles staged by LDS-DMA (global_load_lds_dwordx4) -----------
-// mac3_kernel runs one workgroup per CU (232 VGPRs, 2 waves/SIMD) with ONE tile in flight,
-// staged through registers: 32 KB of B per CU in flight cannot cover HBM latency, and the MAC
-// waits on memory for ~40% of its cycles.  Here the tiles go HBM -> LDS directly (no VGPR
-// cost), in a ring of kMacRing buffers: while tile i is multiplied, tiles i+1 and i+2 are in
-// flight.  A tile's loads are retired by a counted `s_waitcnt vmcnt` (only the loads issued
-// after it may stay outstanding) and a raw s_barrier (a __syncthreads would drain every DMA).
-// LDS images (lane-linear, as LDS-DMA writes them):
-//   B  [tt][col][8 lk]  one 64-B row per (term, column) = the 8 lk of one HBM row;
-//   A  [lk][tt][JP]     the split key rows of one tile, contiguous per lk in As (padded to Tp).
-// Loads per tile: B = 32 wave-instructions (wave w: term w, four 16-column quarters), A = JP/2
-// (wave w < JP/2: 1 KB of the A image).
+// ---- LDS-DMA staging (global_load_lds_dwordx4) ------------------------------------------
+// Register-staged tiles (round 1's mac3_kernel: 232 VGPRs, 2 waves/SIMD, one tile in flight)
+// could not cover HBM latency.  Tiles go HBM -> LDS directly (no VGPR cost), in a ring of
+// kMacRing buffers: while tile i is multiplied, tiles i+1 and i+2 are in flight.  A tile's loads
+// are retired by a counted `s_waitcnt vmcnt` (only the loads issued after it may stay
+// outstanding) and a raw s_barrier (a __syncthreads would drain every DMA).  The removed
+// register-staged and one-column forms are tools/experiments/mac3_mac3g.patch.
 constexpr int kMacRing = 3;
 
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
@@ -913,135 +773,8 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int JP>
-__global__ __launch_bounds__(512, 1) void mac3g_kernel(Mac3Args a) {
-  constexpr int NLK = 8;
-  constexpr int BW = kMac3Tc * 64 * NLK;  // B image words per buffer
-  constexpr int AW = NLK * kMac3Tc * JP;  // A image words per buffer
-  constexpr int NA = JP / 2;              // A wave-instructions per tile
-  constexpr int SW = NLK * kMac3Tc * JP / 2;  // S image (u32 a0 + a1) words per buffer
-  constexpr int NS = (JP + 3) / 4;            // S wave-instructions per tile (16 JP 16-B chunks)
-  constexpr int RW = BW + AW + SW;            // ring words per buffer
-  static_assert(JP * NLK * 64 <= kMacRing * RW, "output stage must fit the ring");
-  __shared__ uint64_t ring[kMacRing * RW];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long long nlkg = a.per_col / NLK;
-  const long long lk0 = (blockIdx.x % nlkg) * NLK, c0 = (blockIdx.x / nlkg) * 64;
-  const int T = a.T1 + a.T2;
-  const int ntile = a.Tp / kMac3Tc;
-  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-  // B loader: wave w stages term w of each tile; quarter k = columns 16k .. 16k+15, lane ->
-  // (column 16k + lane/4, 16-B chunk lane%4 = lk 2(lane%4), +1); clamped addresses past the
-  // last column / term load valid words whose products are discarded (zero key) or unstored
-  const int bq_col = lane >> 2, bq_chunk = lane & 3;
-  auto issue = [&](int tile, int buf) {
-    const uint32_t bbase = ring_lds + (uint32_t)(buf * RW) * 8u;
-    int t = tile * kMac3Tc + w;
-    if (t >= T) t = T - 1;
-    const uint64_t* rowbase = t < a.T1 ? a.B1 + (long long)t * a.b1_term : a.B2 + (long long)(t - a.T1) * a.b2_term;
-    const long long colstride = t < a.T1 ? a.b1_col : a.b2_col;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      long long col = c0 + 16 * k + bq_col;
-      if (col >= a.ncols) col = a.ncols - 1;
-      glds16(rowbase + col * colstride + lk0 + 2 * bq_chunk, bbase + (uint32_t)((w * 64 + 16 * k) * NLK) * 8u);
-    }
-    if (w < NA) {  // A image bytes [1024 w, 1024 w + 1024): lane's 16 B = key words (lk, tt, j..j+1)
-      const int u = (w * 64 + lane) * 2;  // u64 index in [lk][tt][JP]
-      const int lk = u / (kMac3Tc * JP), tt = (u / JP) % kMac3Tc, j = u % JP;
-      glds16(a.As + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc + tt) * JP + j,
-             bbase + (uint32_t)(BW + w * 128) * 8u);
-    }
-    if (w < NS) {  // S image bytes [1024 w, ...): lane's 16 B = four u32 sums (lk, tt, j..j+3)
-      const int c = w * 64 + lane;
-      if (c < 16 * JP) {
-        const int u = 4 * c;  // u32 index in [lk][tt][JP]
-        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
-        glds16(a.Ss + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r,
-               bbase + (uint32_t)(BW + AW) * 8u + (uint32_t)w * 1024u);  // lane-linear: + 16 lane
-      }
-    }
-  };
-  Mac3Acc acc[JP];
-#pragma unroll
-  for (int j = 0; j < JP; ++j) acc[j] = Mac3Acc{0, 0, 0, 0, 0};
-  issue(0, 0);
-  if (ntile > 1) issue(1, 1);
-  int since = 0;
-  for (int it = 0; it < ntile; ++it) {
-    const int buf = it % kMacRing;
-    // this wave's loads of tile `it` are done once only tile it+1's (if issued) are outstanding
-    if (it + 1 < ntile) {
-      if (w < NS) wait_vm<6>();
-      else if (w < NA) wait_vm<5>();
-      else wait_vm<4>();
-    } else {
-      wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();  // every wave's part of tile `it` is in LDS; tile it-1 is consumed
-    if (it + 2 < ntile) issue(it + 2, (it + 2) % kMacRing);
-    const uint64_t* L = ring + buf * RW + lane * NLK + w;
-    const uint64_t* LA = ring + buf * RW + BW + w * (kMac3Tc * JP);
-    const uint32_t* LS = reinterpret_cast<const uint32_t*>(ring + buf * RW + BW + AW) + w * (kMac3Tc * JP);
-#pragma unroll
-    for (int tt = 0; tt < kMac3Tc; ++tt) {
-      const uint64_t b = L[tt * 64 * NLK];
-      const uint32_t b0 = (uint32_t)b & 0x1fffffffu, b1 = (uint32_t)(b >> 29), bs = b0 + b1;
-#pragma unroll
-      for (int j = 0; j < JP; ++j) {
-        const uint64_t av = LA[tt * JP + j];
-        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32), as = LS[tt * JP + j];
-        Mac3Acc& z = acc[j];  // Karatsuba: 3 v_mad_u64_u32 per MAC (s01 holds sm until the fold)
-        z.s00 = mad64(a0, b0, z.s00);
-        z.s01 = mad64(as, bs, z.s01);
-        z.s11 = mad64(a1, b1, z.s11);
-      }
-    }
-    since += kMac3Tc;
-    if (since >= a.fold) {
-#pragma unroll
-      for (int j = 0; j < JP; ++j) mac3k_fold(acc[j]);
-      since = 0;
-    }
-  }
-  __syncthreads();  // every DMA retired (vmcnt(0) above) and every wave done with the ring
-  const int lk = (int)lk0 + w;
-  const RnsPrime& P = a.P[lk / a.d];
-  const uint64_t q = P.q;
-#pragma unroll
-  for (int j = 0; j < JP; ++j) {
-    mac3k_fold(acc[j]);
-    uint64_t r = sh_mul(acc[j].lo, P.rinv, P.rinv_sh, q);
-    r = mod_add(r, sh_mul(acc[j].hi, 1, P.one_sh, q), q);
-    ring[(j * NLK + w) * 64 + lane] = r;  // [j][lk][col]
-  }
-  __syncthreads();
-  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // 8 lk never straddle a limb (d % 8 == 0)
-  for (int pidx = tid; pidx < JP * 64; pidx += 512) {
-    const int c = pidx & 63, j = pidx >> 6;
-    const long long col = c0 + c;
-    if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r[NLK];
-#pragma unroll
-    for (int x = 0; x < NLK; ++x) r[x] = ring[(j * NLK + x) * 64 + c];
-    if (a.C) {
-      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
-#pragma unroll
-      for (int i = 0; i < NLK / 2; ++i) {
-        const ulonglong2 cv = cp[i];
-        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
-        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
-      }
-    }
-    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
-#pragma unroll
-    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
-  }
-}
-
 // ---- mac3h: two columns per lane, half the outputs per wave ----------------------------------
-// mac3g is LDS-bound, not VALU-bound: every MAC needs its key words as a wave-uniform LDS read
+// The one-column form (mac3g, removed) was LDS-bound, not VALU-bound: every MAC needs its key words as a wave-uniform LDS read
 // (12 B: a0 | a1 and a0 + a1), and a uniform ds_read_b128 still costs the LDS 4 cycles, so the
 // key reads of 8 waves alone (3,072 LDS cycles per tile) outrun a SIMD's multiplies (~3,456);
 // its B reads (lane stride 64 B) are 8-way bank conflicts on top.  Here a lane owns TWO
@@ -1214,7 +947,7 @@ static int mac3_jp(int J) {
 static int mac3_fold_period(const RnsPrime* P, int nl) {
   int bits = 29;
   for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
-  // mac3g's Karatsuba middle: (a0 + a1)(b0 + b1) <= smax^2, smax = 2^29 - 1 + max a1 (exact in q)
+  // the Karatsuba middle: (a0 + a1)(b0 + b1) <= smax^2, smax = 2^29 - 1 + max a1 (exact in q)
   double smax = 0;
   for (int l = 0; l < nl; ++l) smax = std::max(smax, (double)((1ull << 29) - 1 + ((P[l].q - 1) >> 29)));
   int f = 32;
@@ -1234,60 +967,21 @@ static bool mac3_ok(const RnsPrime* P, int nl, int J, int T, int d) {
 }
 
 static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
-  const int jp = mac3_jp(m.J);
-  const long long blocks = (m.ncols + 63) / 64 * (m.per_col / 8);
-  const dim3 g((unsigned)blocks), b(512);
-  static int regstage = -1;  // RINGO_MAC3=r / g: mac3_kernel / mac3g_kernel (comparison runs)
-  if (regstage < 0) {
-    const char* e = getenv("RINGO_MAC3");
-    regstage = (e && e[0] == 'r') ? 1 : (e && e[0] == 'g') ? 2 : (e && e[0] == '2') ? 3 : 0;  // r: mac3, g: mac3g, 2: mac3h<JP,2>
+  // mac3h, 4 output groups (1,024 threads) where JP allows, 2 otherwise
+  const dim3 gh((unsigned)((m.ncols + 127) / 128 * (m.per_col / 4)));
+  const dim3 b2(512), b4(1024);
+  switch (mac3_jp(m.J)) {
+    case 4: hipLaunchKernelGGL((mac3h_kernel<4, 2>), gh, b2, 0, st, m); break;
+    case 6: hipLaunchKernelGGL((mac3h_kernel<6, 2>), gh, b2, 0, st, m); break;
+    case 8: hipLaunchKernelGGL((mac3h_kernel<8, 4>), gh, b4, 0, st, m); break;
+    case 10: hipLaunchKernelGGL((mac3h_kernel<10, 2>), gh, b2, 0, st, m); break;
+    case 12: hipLaunchKernelGGL((mac3h_kernel<12, 4>), gh, b4, 0, st, m); break;
+    default: hipLaunchKernelGGL((mac3h_kernel<16, 4>), gh, b4, 0, st, m); break;
   }
-  if (regstage == 0 || regstage == 3) {  // default: mac3h, 4 output groups where JP allows (3: 2 groups)
-    const dim3 gh((unsigned)((m.ncols + 127) / 128 * (m.per_col / 4)));
-    const dim3 b2(512), b4(1024);
-    const bool g4 = regstage == 0;
-    switch (jp) {
-      case 4: hipLaunchKernelGGL((mac3h_kernel<4, 2>), gh, b2, 0, st, m); break;
-      case 6: hipLaunchKernelGGL((mac3h_kernel<6, 2>), gh, b2, 0, st, m); break;
-      case 8:
-        if (g4) hipLaunchKernelGGL((mac3h_kernel<8, 4>), gh, b4, 0, st, m);
-        else hipLaunchKernelGGL((mac3h_kernel<8, 2>), gh, b2, 0, st, m);
-        break;
-      case 10: hipLaunchKernelGGL((mac3h_kernel<10, 2>), gh, b2, 0, st, m); break;
-      case 12:
-        if (g4) hipLaunchKernelGGL((mac3h_kernel<12, 4>), gh, b4, 0, st, m);
-        else hipLaunchKernelGGL((mac3h_kernel<12, 2>), gh, b2, 0, st, m);
-        break;
-      default:
-        if (g4) hipLaunchKernelGGL((mac3h_kernel<16, 4>), gh, b4, 0, st, m);
-        else hipLaunchKernelGGL((mac3h_kernel<16, 2>), gh, b2, 0, st, m);
-        break;
-    }
-    return check_launch("jindo mac3h");
-  }
-  if (regstage == 2) {
-    switch (jp) {
-      case 4: hipLaunchKernelGGL((mac3g_kernel<4>), g, b, 0, st, m); break;
-      case 6: hipLaunchKernelGGL((mac3g_kernel<6>), g, b, 0, st, m); break;
-      case 8: hipLaunchKernelGGL((mac3g_kernel<8>), g, b, 0, st, m); break;
-      case 10: hipLaunchKernelGGL((mac3g_kernel<10>), g, b, 0, st, m); break;
-      case 12: hipLaunchKernelGGL((mac3g_kernel<12>), g, b, 0, st, m); break;
-      default: hipLaunchKernelGGL((mac3g_kernel<16>), g, b, 0, st, m); break;
-    }
-    return check_launch("jindo mac3g");
-  }
-  switch (jp) {
-    case 4: hipLaunchKernelGGL((mac3_kernel<4, 1>), g, b, 0, st, m); break;
-    case 6: hipLaunchKernelGGL((mac3_kernel<6, 1>), g, b, 0, st, m); break;
-    case 8: hipLaunchKernelGGL((mac3_kernel<8, 1>), g, b, 0, st, m); break;
-    case 10: hipLaunchKernelGGL((mac3_kernel<10, 1>), g, b, 0, st, m); break;
-    case 12: hipLaunchKernelGGL((mac3_kernel<12, 1>), g, b, 0, st, m); break;
-    default: hipLaunchKernelGGL((mac3_kernel<16, 1>), g, b, 0, st, m); break;
-  }
-  return check_launch("jindo mac3");
+  return check_launch("jindo mac3h");
 }
 
-// the commit key of one MAC, split and transposed for mac3_kernel (on the device):
+// the commit key of one MAC, split and transposed for mac3h_kernel (on the device):
 // out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J and terms
 // t >= T1 + T2, up to the padded count Tp, zero)
 __global__ __launch_bounds__(256) void mac3_key_kernel(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J,
@@ -1479,25 +1173,10 @@ struct SampleArgs {
   long long* mlwe_noise;  // [B][cols+1][nm][d]
   long long n_enc_pairs, n_ml_pairs;
   long long batch;
-  // TwinCDT v0 != v1 tails deferred by cdt_noise_kernel to cdt_tail_kernel: one segment of
-  // tail_cap entries per wave, entry counts in tail_n
-  struct CdtTail* tails;
-  int* tail_n;
-  long long tail_cap;
   // cdt2_noise_kernel's tail bounds: [129][size + 2], row c, entry j + 1 = the reference's tail
   // cdf sum_{x = tailLo}^{j} rho(x - c/128) / norm for j = -1 .. size (host, Go's order)
   const double* cdt_sbound;
   const int* cdt_jmax;  // [128]: v0 <= jmax[c0] decides the sample as v0 (cdt2_noise_kernel)
-};
-
-// a TwinCDT sample whose two table searches disagree (twin_cdt.go:95-110): enc_noise[out]
-// holds v1's result; it becomes `alt` (v0's) when u / 2^64 < the exp-sum cdf over x <= v0
-struct CdtTail {
-  unsigned long long out;
-  uint64_t u;
-  double c_frac;
-  long long alt;
-  long long v0;
 };
 
 #pragma clang fp contract(off)
@@ -1519,56 +1198,16 @@ __device__ __forceinline__ double enc_centre(const SampleArgs& a, const uint32_t
 }
 #pragma clang fp contract(on)
 
-// thread = (commit, column, row, coefficient pair): Gaussian samples of one randEncodeTo
-__global__ __launch_bounds__(512) void enc_noise_kernel(SampleArgs a) {
-  __shared__ uint32_t lds[kAesLds];
-  __shared__ uint32_t keys[2][kKeyWords];
-  aes_lds_fill(lds, a.te0);
-  aes_key_fill(keys[0], a.key[kDomCosac]);
-  aes_key_fill(keys[1], a.key[kDomCosacRnd]);
-  __syncthreads();
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= a.n_enc_pairs) return;
-  const JShape& S = a.s;
-  const int m = (int)(gid % (S.d / 2));
-  const long long poly = gid / (S.d / 2);  // (b, col, row) flattened
-  const int row = (int)(poly % S.rows), col = (int)((poly / S.rows) % (S.cols + 1));
-  long long* out = a.enc_noise + poly * S.d;
-  if (enc_skipped(S, col, row)) {  // the reference draws nothing for these (prover.go:101-105,118-123)
-    out[2 * m] = 0;
-    out[2 * m + 1] = 0;
-    return;
-  }
-  const uint32_t* dg = a.digits + poly * S.d;
-  const double sd = col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
-  const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
-  if (sd == a.sd_ecd) {  // Encoder.twinCDT (encoder.go:169-170): one word per sample
-    uint64_t w0, w1;
-    ks_words(a.key[kDomEncCdt], gpoly, (uint64_t)m, lds, w0, w1);
-    out[2 * m] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m), w0);
-    out[2 * m + 1] = twin_cdt(a.cdt_enc, enc_centre(a, dg, 2 * m + 1), w1);
-  } else {  // Encoder.cosac (encoder.go:171-172): thread m < d / G draws group m's G samples in order
-    const int G = S.d < kCosGroup ? S.d : kCosGroup;
-    if (m < S.d / G) {
-      Uniform base, rnd;
-      base.init(keys[0], lds, gpoly * (unsigned long long)(S.d / G) + (unsigned long long)m);
-      rnd.init(keys[1], lds, gpoly * (unsigned long long)(S.d / G) + (unsigned long long)m);
-      for (int k = m * G; k < (m + 1) * G; ++k) out[k] = cosac(a.zig, base, rnd, enc_centre(a, dg, k), sd);
-    }
-  }
-}
-
 // ---- d = 256 encode noise, split by sampler -----------------------------------------------
-// enc_noise_kernel above runs both samplers in one grid and every sample's slow path inline,
-// so a wave waits for its slowest lane: the TwinCDT exp tail (v0 != v1: ~1/128 of samples, up
-// to |tail_lo| + v0 + 1 exp terms) and COSAC's rejection loop (max over 64 lanes of a ~50%
-// acceptance geometric).  The kernels below draw the same words from the same instances, so
-// their output is identical:
+// One kernel per sampler, so a wave never waits on the other sampler's slow path:
 //   cdt2_noise_kernel   wave per TwinCDT polynomial, 4 coefficients per lane (2 AES blocks);
 //                       digits staged in LDS for the deltaInv centres; one guide-table lookup
-//                       per sample (cdt_noise_kernel + cdt_tail_kernel: the round-2 form, kept
-//                       behind RINGO_CDT=legacy);
+//                       per sample; tails decided inline;
 //   cosac2_noise_kernel COSAC groups as a work queue through one state machine.
+// The sampling entry points refuse shapes these kernels do not cover (d != 256, slots % 4 != 0,
+// TwinCDT tables above kCdtLdsMaxSize entries: fields with exp >= 128, or caller stddevs far above
+// NewParameters').  The round-2 kernels that covered them (enc_noise_kernel, cdt_noise_kernel +
+// cdt_tail_kernel) are tools/experiments/legacy_samplers.patch.
 // profiling variants' stand-in keystream (never in a production build)
 __device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -1582,7 +1221,6 @@ __device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
                   // 64 cosac2 without libm exp / log (cheap stand-ins: cost of the rare branches)
 #endif
 #pragma clang fp contract(off)
-constexpr int kCdtWaves = 16;       // waves per cdt_noise_kernel workgroup (one workgroup per CU)
 constexpr int kCdtLdsMaxSize = 96;  // tables' high words + guide in LDS when size <= 96 (<= 145 KiB
                                     // per workgroup with the 64 KiB AES table)
 constexpr int kCdtChunk = 32;       // consecutive polynomials per chunk
@@ -1614,260 +1252,16 @@ __device__ __forceinline__ int cdt_search_hi(const uint32_t* hi, const uint64_t*
   return eq ? lo - 1 : lo;
 }
 
-// lower_bound searches of a lane's 4 samples in tables c0 and c1 (8 searches).  LdsTable: a
-// guide table (per table, the lower_bound of t * 2^56 for t = 0..256, u8) narrows each search
-// to the entries sharing u's top byte, mostly 0-2 of them, then a bisection over that range
-// on the tables' high words in LDS (the full word from global memory only on a tie).
-// Otherwise: plain bisection of the global tables.
-template <bool LdsTable>
-__device__ __forceinline__ void cdt_search8(const uint32_t* thi, const uint8_t* guide, const CdtDev& C, const int tab[8],
-                                            const uint64_t u[4], int res[8]) {
-  const int n = C.size;
-  auto less = [&](int j, int idx) {
-    const uint64_t uj = u[j >> 1];
-    const long long o = (long long)tab[j] * n + idx;
-    if (!LdsTable) return C.tables[o] < uj;
-    const uint32_t th = thi[o], uh = (uint32_t)(uj >> 32);
-    return th != uh ? th < uh : C.tables[o] < uj;  // a tie of the high words: the full word
-  };
-  int lo[8], len[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (LdsTable) {
-      const int t = (int)(u[j >> 1] >> 56);
-      lo[j] = guide[tab[j] * 257 + t];
-      len[j] = guide[tab[j] * 257 + t + 1] - lo[j];  // answer in [lo, lo + len]
-    } else {
-      lo[j] = 0;
-      len[j] = n;
-    }
-  }
-  for (;;) {
-    bool more = false;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (len[j] > 0) {
-        const int half = len[j] >> 1;
-        if (less(j, lo[j] + half)) {
-          lo[j] += half + 1;
-          len[j] -= half + 1;
-        } else {
-          len[j] = half;
-        }
-        more |= len[j] > 0;
-      }
-    if (!__ballot(more)) break;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int i = lo[j];  // lower_bound; found -> index - 1 (slices.BinarySearch)
-    const uint64_t uj = u[j >> 1];
-    const long long o = (long long)tab[j] * n + i;
-    bool eq = false;
-    if (i < n) eq = (LdsTable ? thi[o] == (uint32_t)(uj >> 32) : true) && C.tables[o] == uj;
-    res[j] = eq ? i - 1 : i;
-  }
-}
-
-__device__ __forceinline__ double wave_sum_f64(double x) {
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
-  return x;
-}
-
-// dynamic LDS of cdt_noise_kernel<true>: high words [128][size] u32, guide [128][257] u8, key
+// dynamic LDS of cdt2_noise_kernel: high words [128][size] u32, guide [128][257] u8, key, then
+// the waves' digit slots and jmax
 __host__ __device__ constexpr int cdt_guide_off(int size) { return 128 * size * 4; }
 __host__ __device__ constexpr int cdt_key_off(int size) { return cdt_guide_off(size) + ((128 * 257 + 3) & ~3); }
-__host__ __device__ constexpr int cdt_dyn_lds(bool lds_table, int size) {
-  return lds_table ? cdt_key_off(size) + kKeyWords * 4 : kKeyWords * 4;
-}
 
+// ---- cdt2: TwinCDT for every encode polynomial, tails decided inline ----------------------
 // Each wave owns a contiguous range of the batch's (commit, column, row) polynomials: TwinCDT
 // polynomials are sampled; COSAC ones get their deltaInv centres (as doubles, in enc_noise)
 // for cosac2_noise_kernel; skipped ones are zeroed.
-template <bool LdsTable>
-__global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a) {
-  __shared__ uint32_t lds[kAesLds];
-  extern __shared__ uint32_t dyn[];
-  const CdtDev& C = a.cdt_enc;
-  uint32_t* thi = dyn;
-  uint8_t* guide = reinterpret_cast<uint8_t*>(dyn) + cdt_guide_off(C.size);
-  uint32_t* keyl = LdsTable ? dyn + cdt_key_off(C.size) / 4 : dyn;
-  aes_lds_fill(lds, a.te0);
-  aes_key_fill(keyl, a.key[kDomEncCdt]);
-  if (LdsTable) {
-    for (int i = threadIdx.x; i < 128 * C.size; i += blockDim.x) thi[i] = (uint32_t)(C.tables[i] >> 32);
-    for (int i = threadIdx.x; i < 128 * 257; i += blockDim.x) guide[i] = C.guide[i];
-  }
-  __syncthreads();
-  const JShape& S = a.s;
-  const int lane = threadIdx.x & 63;
-  const long long npoly = a.batch * (S.cols + 1) * S.rows;
-  const long long nw = (long long)gridDim.x * kCdtWaves;
-  const double norm = sqrt(2.0 * M_PI) * C.sigma;
-  const double two_s2 = 2.0 * C.sigma * C.sigma;
-  const LdsKey key{keyl};
-  const long long wv = (long long)blockIdx.x * kCdtWaves + (threadIdx.x >> 6);
-  CdtTail* seg = a.tails + wv * a.tail_cap;
-  long long ntail = 0;
-  // chunks of kCdtChunk consecutive polynomials, dealt round-robin to the waves
-  for (long long p0 = ((long long)blockIdx.x * kCdtWaves + (threadIdx.x >> 6)) * kCdtChunk; p0 < npoly;
-       p0 += nw * kCdtChunk) {
-  const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
-  int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
-  for (long long poly = p0; poly < p1; ++poly) {  // (b, col, row) flattened
-    if (poly > p0 && ++row == S.rows) {
-      row = 0;
-      if (++col == S.cols + 1) col = 0;
-    }
-    long long* out = a.enc_noise + poly * 256;
-    if (enc_skipped(S, col, row)) {  // the reference draws nothing for these (prover.go:101-105,118-123)
-      reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(0, 0);
-      reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(0, 0);
-      continue;
-    }
-    const double sd =
-        col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
-    const bool cdt = sd == a.sd_ecd;
-    const uint32_t* dg = a.digits + poly * 256;
-    // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order)
-    double fp[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = 0; i < S.exp; ++i) {
-      const double di = a.delta[i];
-      if (di == 0.0) continue;
-      const int base = 4 * lane + (i + 1) * S.slots;  // coefficient k reads digit (k + (i+1) slots) mod 256
-      const uint4 g = *reinterpret_cast<const uint4*>(dg + (base & 255));
-      const uint32_t gv[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        if (base + h >= 256)
-          fp[h] = fp[h] + di * (double)gv[h];
-        else
-          fp[h] = fp[h] - di * (double)gv[h];
-      }
-    }
-    if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
-      reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
-      reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
-      continue;
-    }
-    const unsigned long long gpoly =
-        a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
-    uint64_t u[4];
-#if RG_VAR & 2
-    for (int h = 0; h < 4; ++h) u[h] = (gpoly * 0x9E3779B97F4A7C15ull + (uint64_t)(4 * lane + h)) * 0xBF58476D1CE4E5B9ull;
-#else
-    ks_words(key, gpoly, (uint64_t)(2 * lane), lds, u[0], u[1]);
-    ks_words(key, gpoly, (uint64_t)(2 * lane + 1), lds, u[2], u[3]);
-#endif
-    // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111)
-    int tab[8], v[8];
-    double cf[4], flo[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const double center = -fp[h];
-      flo[h] = floor(center);
-      cf[h] = center - flo[h];
-      tab[2 * h] = (int)((int64_t)floor(128.0 * cf[h]) % 128);
-      tab[2 * h + 1] = (int)((int64_t)ceil(128.0 * cf[h]) % 128);
-    }
-#if RG_VAR & 4
-    for (int j = 0; j < 8; ++j) v[j] = (int)(u[j >> 1] >> 58) + (j & 1);
-#else
-    cdt_search8<LdsTable>(thi, guide, C, tab, u, v);
-#endif
-    int64_t res[4];
-    uint32_t pend = 0;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      res[h] = (int64_t)v[2 * h + 1] + C.tail_lo + (int64_t)flo[h];
-      if (v[2 * h] != v[2 * h + 1]) pend |= 1u << h;
-    }
-#if RG_VAR & 1
-    pend = 0;
-#endif
-    // the v0 != v1 tails: appended to this wave's segment for cdt_tail_kernel (counts <= 4 per
-    // lane: offsets from three ballots of the count's bits); only if the segment is full are they
-    // resolved here, one at a time across the wave: lanes compute the exp terms, a tree sum
-    // decides p < cdf unless p is within the two sums' error bound of it, and only then the
-    // terms are summed in the reference's order (readlane chain)
-    {
-      const int cnt = __builtin_popcount(pend);
-      const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
-      const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
-      if (tot && ntail + tot <= a.tail_cap) {
-        auto mb = [](uint64_t m) {
-          return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        };
-        long long o = ntail + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-          if (pend & (1u << h)) {
-            CdtTail t;
-            t.out = (unsigned long long)(poly * 256 + 4 * lane + h);
-            t.u = u[h];
-            t.c_frac = cf[h];
-            t.alt = (int64_t)v[2 * h] + C.tail_lo + (int64_t)flo[h];
-            t.v0 = v[2 * h];
-            seg[o++] = t;
-          }
-        ntail += tot;
-        pend = 0;
-      }
-    }
-    for (;;) {
-      const uint64_t any = __ballot(pend != 0);
-      if (!any) break;
-      const int src = __builtin_amdgcn_readfirstlane(__builtin_ctzll(any));
-      const int hs = __builtin_amdgcn_readlane(pend ? __builtin_ctz(pend) : 0, src);
-      double c_frac = 0.0, p = 0.0;
-      int v0 = 0;
-#pragma unroll
-      for (int h = 0; h < 4; ++h)
-        if (h == hs) {
-          c_frac = cf[h];
-          v0 = v[2 * h];
-          p = __ull2double_rn(u[h]) / 18446744073709551616.0;
-        }
-      c_frac = rl_f64(c_frac, src);
-      v0 = __builtin_amdgcn_readlane(v0, src);
-      const int nterm = (int)((int64_t)v0 - C.tail_lo + 1);
-      double approx = 0.0;
-      for (int64_t x0 = C.tail_lo; x0 <= v0; x0 += 64) {
-        const double xf = (double)(x0 + lane);
-        const double term = x0 + lane <= v0 ? exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm : 0.0;
-        approx += wave_sum_f64(term);
-      }
-      // |tree sum - sequential sum| <= 2 (n-1) 2^-53 sum (+ a margin)
-      const double bound = approx * (4.0 * (nterm + 2)) * 1.1102230246251565e-16;
-      bool lt = p < approx;
-      const bool close = fabs(p - approx) <= bound;
-      if (__builtin_amdgcn_readlane((int)close, src)) {
-        double cdf = 0.0;
-        for (int64_t x0 = C.tail_lo; x0 <= v0; x0 += 64) {
-          const double xf = (double)(x0 + lane);
-          const double term = exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm;
-          const int nn = (int)std::min<int64_t>(64, (int64_t)v0 - x0 + 1);
-          for (int i = 0; i < nn; ++i) cdf += rl_f64(term, i);
-        }
-        lt = p < cdf;
-      }
-      if (lane == src) {
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-          if (h == hs && lt) res[h] = (int64_t)v[2 * h] + C.tail_lo + (int64_t)flo[h];
-        pend &= pend - 1;
-      }
-    }
-    reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(res[0], res[1]);
-    reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(res[2], res[3]);
-  }
-  }
-  if (lane == 0) a.tail_n[wv] = (int)ntail;
-}
-
-// ---- cdt2: TwinCDT for every encode polynomial, tails decided inline ----------------------
-// cdt_noise_kernel<true> spends its time on (round-2 profiling variants) the deltaInv centres,
+// The round-2 form (cdt_noise_kernel) spent its time on (profiling variants) the deltaInv centres,
 // 16 dependent global loads per polynomial, and eight table searches per lane; its v0 != v1
 // tails go to a second kernel that sums up to 2 tailHi + 1 exp terms each.  Here:
 //  * the polynomial's 256 digits are staged in a wave-private 1 KiB LDS slot (one 16-B store per
@@ -1881,8 +1275,7 @@ __global__ __launch_bounds__(64 * kCdtWaves) void cdt_noise_kernel(SampleArgs a)
 //    so S[c0 + 1][v0] (1 - 2^-40) <= cdf <= S[c0][v0] (1 + 2^-40) (S summed on the host in the same
 //    order; 2^-40 covers both libms and the float sums).  Outside that band the comparison is
 //    decided; inside it (p within 1e-12 of the sum: p ~ 1, unseen in practice) the wave sums the
-//    terms in the reference's order, as cdt_noise_kernel does.  Results equal the reference's
-//    draw for draw; cdt_tail_kernel is not needed.
+//    terms in the reference's order.  Results equal the reference's draw for draw.
 constexpr int kCdt2Waves = 16;
 __host__ __device__ constexpr int cdt2_dig_off(int size) { return cdt_key_off(size) + kKeyWords * 4; }
 __host__ __device__ constexpr int cdt2_jmax_off(int size) { return cdt2_dig_off(size) + kCdt2Waves * 1024; }
@@ -2072,50 +1465,6 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       reinterpret_cast<longlong2*>(out)[2 * lane] = make_longlong2(res[0], res[1]);
       reinterpret_cast<longlong2*>(out)[2 * lane + 1] = make_longlong2(res[2], res[3]);
     }
-  }
-}
-
-// The deferred TwinCDT tails: wave w resolves segment w, two entries at a time (32 lanes each):
-// each lane sums its share of the exp terms, a 32-lane tree sum decides p < cdf unless p lies
-// within the error bound of both sums, then the terms are summed in the reference's order.
-constexpr int kTailWavesPerSeg = 4;  // waves sharing one segment (latency hiding)
-__global__ __launch_bounds__(256) void cdt_tail_kernel(SampleArgs a) {
-  const CdtDev& C = a.cdt_enc;
-  const long long wv = blockIdx.x;  // segment; its 4 waves take pairs w, w + 4, ...
-  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31, w = threadIdx.x >> 6;
-  const int n = a.tail_n[wv];
-  const CdtTail* seg = a.tails + wv * a.tail_cap;
-  const double norm = sqrt(2.0 * M_PI) * C.sigma;
-  const double two_s2 = 2.0 * C.sigma * C.sigma;
-  for (int e0 = 2 * w; e0 < n; e0 += 2 * kTailWavesPerSeg) {
-    const int e = e0 + half < n ? e0 + half : e0;
-    const CdtTail t = seg[e];
-    double part = 0.0;
-    for (long long x = C.tail_lo + hl; x <= t.v0; x += 32) {
-      const double xf = (double)x;
-      part += exp(-(xf - t.c_frac) * (xf - t.c_frac) / two_s2) / norm;
-    }
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) part += __shfl_xor(part, m, 64);
-    const double p = __ull2double_rn(t.u) / 18446744073709551616.0;
-    const int nterm = (int)(t.v0 - C.tail_lo + 1);
-    const double bound = part * (4.0 * (nterm + 2)) * 1.1102230246251565e-16;
-    bool lt = p < part;
-    const bool close = fabs(p - part) <= bound;
-    for (int hh = 0; hh < 2; ++hh) {  // exact sums (rare), one entry at a time across the wave
-      if (!__builtin_amdgcn_readlane((int)close, 32 * hh)) continue;
-      const double c_frac = rl_f64(t.c_frac, 32 * hh);
-      const long long v0 = (long long)__builtin_amdgcn_readlane((int)t.v0, 32 * hh);
-      double cdf = 0.0;
-      for (long long x0 = C.tail_lo; x0 <= v0; x0 += 64) {
-        const double xf = (double)(x0 + lane);
-        const double term = exp(-(xf - c_frac) * (xf - c_frac) / two_s2) / norm;
-        const int nn = (int)std::min<long long>(64, v0 - x0 + 1);
-        for (int i = 0; i < nn; ++i) cdf += rl_f64(term, i);
-      }
-      if (half == hh) lt = p < cdf;
-    }
-    if (hl == 0 && e0 + half < n && lt) a.enc_noise[t.out] = t.alt;
   }
 }
 
@@ -2735,7 +2084,6 @@ __global__ __launch_bounds__(256) void dot2_kernel(FieldParams<L> F, const uint6
 struct rg_jindo_scratch {
   rg::DevBuf digits, com, ocom;
   rg::DevBuf last, mask, en, mn;  // the sampled randomness of rg_jindo_commit_sampled_dev
-  rg::DevBuf tails, tail_n;       // deferred TwinCDT tails (cdt_noise_kernel -> cdt_tail_kernel)
 };
 
 // Sampler setup (rg_jindo_set_stddevs): the reference's six standard deviations and the tables
@@ -2758,7 +2106,7 @@ struct rg_jindo {
   rg::CrtDev crt_q, crt_o;
   rg::DstDev dst_o, dst_q;
   rg::DevBuf ck_in, ck_mlwe, ck_out;  // the commit key, device-resident (entities.go:21-73 layouts)
-  rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3_kernel (inner, outer)
+  rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3h_kernel (inner, outer; built only where it runs)
   bool mac3_q = false, mac3_o = false;
   rg::DevBuf ckm_in, ckm_out;  // the same as base-256 digits for mac_mfma (inner, outer)
   int mfma_q = 0, mfma_o = 0;  // digits per residue of the MFMA MAC (0: mac3h / mac_kernel)
@@ -3035,7 +2383,7 @@ static rg_status stream_scratch(rg_jindo* J, size_t batch, hipStream_t st, rg_ji
 static bool prep_legacy() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("RINGO_JINDO_PREP");
+    const char* e = knob(Knob::JindoPrep);
     v = (e && e[0] == 'l') ? 1 : 0;
   }
   return v == 1;
@@ -3230,7 +2578,7 @@ static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const 
   for (int l = 0; l < nq; ++l) q61 = q61 && J->rq[l].q < (1ull << 61);
   if (d == 256 && q61 && !prep_legacy()) {
     static const int pw = [] {  // RINGO_JINDO_PREP_W: minimum waves per SIMD for prep256 (tuning)
-      const char* e = getenv("RINGO_JINDO_PREP_W");
+      const char* e = knob(Knob::JindoPrepW);
       return e ? atoi(e) : 6;
     }();
     const dim3 g((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
@@ -3323,6 +2671,15 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     set_last_error("rg_jindo_set_stddevs was not called on this handle");
     return RG_ERR_INVALID;
   }
+  const rg_jindo_samplers& S = J->smp;
+  // the shapes the device samplers cover (every NewParameters shape of a field with exp <= 64)
+  if (p.d != 256 || p.slots % 4 != 0 || S.cdt_enc_size > kCdtLdsMaxSize ||
+      cdt2_dyn_lds(S.cdt_enc_size) + (int)sizeof(uint32_t) * kAesLds > 163840) {
+    set_last_error("device sampling needs d = 256, slots % 4 == 0 and an encode TwinCDT table of <= 96 entries (got d = " +
+                   std::to_string(p.d) + ", slots = " + std::to_string(p.slots) + ", table " +
+                   std::to_string(S.cdt_enc_size) + ")");
+    return RG_ERR_UNSUPPORTED;
+  }
   SampleArgs a;
   memset(&a, 0, sizeof(a));
   RG_TRY(make_keys(seeds, a.key));
@@ -3336,7 +2693,6 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   }
   RG_TRY(s);
   RG_TRY(digits_stage(J, batch, d_v, nv, d_last, d_mask, digits, st));
-  const rg_jindo_samplers& S = J->smp;
   a.s = shape_of(p, (long long)nv);
   a.te0 = S.te0.as<uint32_t>();
   a.first_commit = first;
@@ -3357,49 +2713,18 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   a.n_enc_pairs = (long long)batch * (p.cols + 1) * p.rows * (p.d / 2);
   a.n_ml_pairs = (long long)batch * (p.cols + 1) * nm * (p.d / 2);
   a.batch = (long long)batch;
-  if (p.d == 256) {
+  {
     const long long npoly = (long long)batch * (p.cols + 1) * p.rows;
-    const unsigned g = (unsigned)std::min<long long>((npoly + kCdtWaves - 1) / kCdtWaves, 256);
-    // tail segments: 1/64 of a wave's samples (TwinCDT tails run near 1/128) + 256
-    const long long nw = (long long)g * kCdtWaves;
-    const long long chunks = (npoly + kCdtChunk - 1) / kCdtChunk;
-    a.tail_cap = (chunks + nw - 1) / nw * kCdtChunk * 256 / 64 + 256;
-    {
-      std::lock_guard<std::mutex> lk(J->mu);
-      const size_t tb = (size_t)(nw * a.tail_cap) * sizeof(CdtTail), nb = (size_t)nw * sizeof(int);
-      if (sc->tails.bytes < tb || sc->tail_n.bytes < nb) RG_HIP(hipStreamSynchronize(st));
-      RG_TRY(sc->tails.alloc(tb));
-      RG_TRY(sc->tail_n.alloc(nb));
-    }
-    a.tails = sc->tails.as<CdtTail>();
-    a.tail_n = sc->tail_n.as<int>();
+    const unsigned g = (unsigned)std::min<long long>((npoly + kCdt2Waves - 1) / kCdt2Waves, 256);
     a.cdt_sbound = S.cdt_sbound.as<double>();
     a.cdt_jmax = S.cdt_jmax.as<int>();
-    static const bool cdt_legacy = [] {  // RINGO_CDT=legacy: cdt_noise_kernel + cdt_tail_kernel (A/B)
-      const char* e = getenv("RINGO_CDT");
-      return e && e[0] == 'l';
-    }();
-    if (!cdt_legacy && S.cdt_enc_size <= kCdtLdsMaxSize && p.slots % 4 == 0 &&
-        cdt2_dyn_lds(S.cdt_enc_size) + (int)sizeof(uint32_t) * kAesLds <= 163840) {
-      hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
-      RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
-    } else {
-    if (S.cdt_enc_size <= kCdtLdsMaxSize)
-      hipLaunchKernelGGL(cdt_noise_kernel<true>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(true, S.cdt_enc_size), st, a);
-    else
-      hipLaunchKernelGGL(cdt_noise_kernel<false>, dim3(g), dim3(64 * kCdtWaves), cdt_dyn_lds(false, 0), st, a);
+    hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
-    hipLaunchKernelGGL(cdt_tail_kernel, dim3((unsigned)nw), dim3(64 * kTailWavesPerSeg), 0, st, a);
-    RG_TRY(check_launch("jindo enc noise (TwinCDT tails)"));
-    }
     const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
     const long long w2 = kCos2Threads / 64;
     const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
     hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (COSAC)"));
-  } else {
-    hipLaunchKernelGGL(enc_noise_kernel, dim3((unsigned)((a.n_enc_pairs + 511) / 512)), dim3(512), 0, st, a);
-    RG_TRY(check_launch("jindo enc noise"));
   }
   hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)std::min<long long>((a.n_ml_pairs + 511) / 512, 1024)), dim3(512),
                      0, st, a);
@@ -3826,15 +3151,16 @@ static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** 
 }
 
 // The commit key is device-resident from here on: ck_in/ck_mlwe/ck_out hold it in the
-// entities.go layouts; mac3's split + transposed copies are built from them on the device.
+// entities.go layouts; the MAC kernels' key images (MFMA digits, or mac3h's split + transposed
+// words) are built from them on the device, only for the MAC each product runs on.
 static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
   const rg_jindo_params& p = J->p;
-  const bool legacy = getenv("RINGO_JINDO_MAC") && getenv("RINGO_JINDO_MAC")[0] == 'l';  // A/B switch
+  // RINGO_JINDO_MAC (experiments build): l = mac_kernel, h = mac3h (VALU); default = the MFMA MAC
+  // where it applies, else mac3h where it applies, else mac_kernel
+  const char* mk = knob(Knob::JindoMac);
+  const bool legacy = mk && mk[0] == 'l';
+  const bool no_mfma = legacy || (mk && mk[0] == 'h');
   const size_t pcq = (size_t)p.nq * p.d, pco = (size_t)p.nqo * p.d;
-  J->mac3_q = !legacy && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
-  J->mac3_o = !legacy && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
-  // RINGO_JINDO_MAC: l = mac_kernel, h = mac3h (VALU), default = the MFMA MAC where it applies
-  const bool no_mfma = legacy || (getenv("RINGO_JINDO_MAC") && getenv("RINGO_JINDO_MAC")[0] == 'h');
   {
     uint64_t pq[kMaxQ], po[kMaxQ];
     MfmaPrime mq[kMaxQ], mo[kMaxQ];
@@ -3849,6 +3175,8 @@ static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
       RG_TRY(mac_mfma_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, (long long)pco, p.d,
                               J->mfma_o, mo, p.nqo, J->ckm_out, st));
   }
+  J->mac3_q = !legacy && !J->mfma_q && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
+  J->mac3_o = !legacy && !J->mfma_o && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
   if (J->mac3_q)
     RG_TRY(mac3_key_dev(J->ck_in.as<uint64_t>(), p.rows, J->ck_mlwe.as<uint64_t>(), p.mlwe, p.in_msis, pcq, J->ck3_in, st));
   if (J->mac3_o) RG_TRY(mac3_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, pco, J->ck3_out, st));
@@ -4200,7 +3528,7 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   // scratch) belongs to this caller stream only, so concurrent callers on different streams never
   // share a buffer.
   static const bool no_split = [] {  // RINGO_JINDO_SPLIT=0: one stream (per-kernel profiling)
-    const char* e = getenv("RINGO_JINDO_SPLIT");
+    const char* e = knob(Knob::JindoSplit);
     return e && e[0] == '0';
   }();
   if (batch < 64 || no_split) return run(0, batch, st);
@@ -4240,6 +3568,13 @@ rg_status rg_jindo_release_stream(rg_jindo* J, void* stream) {
     J->aux.erase(a);
   }
   J->scratch.erase(st);
+  return RG_OK;
+}
+
+rg_status rg_jindo_mac_kinds(const rg_jindo* J, int* inner, int* outer) {
+  if (!J || !inner || !outer) return RG_ERR_INVALID;
+  *inner = J->mfma_q ? RG_MAC_MFMA : J->mac3_q ? RG_MAC_VALU3 : RG_MAC_GENERIC;
+  *outer = J->mfma_o ? RG_MAC_MFMA : J->mac3_o ? RG_MAC_VALU3 : RG_MAC_GENERIC;
   return RG_OK;
 }
 

@@ -243,7 +243,10 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
 #endif
 // LOGN = 16 (COL and ROW both 8-stage passes) or 15 (COL: 7 stages on 256 columns of 128 points,
 // 8 of them per tile; ROW: 8 stages on 128 rows of 256 points), as ntt.hip plans them.
-template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int LOGN = 16>
+// PROBE (experiments build only, rg_set_probe(5); production = 0): 1 = no HBM data movement,
+// the tile synthesised in registers and the result kept live by a store that never fires, so the
+// same launch times the butterflies, twiddle loads and LDS exchanges alone.
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int LOGN = 16, int PROBE = 0>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_WPE))) void ntt256_pass(Ntt256Args a) {
   static_assert(LOGN == 15 || LOGN == 16, "ntt256_pass: N = 2^15 or 2^16");
   constexpr int LOGC = COL ? LOGN - 8 : 8;        // bits of a sub-transform
@@ -272,6 +275,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
   uint32_t e[8][8];
   auto gload = [&](int reg, uint32_t x) {
     const uint32_t off = ((s << SSH) + (x << XSH)) * 32u;
+    if constexpr (PROBE != 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[reg][i] = (off + (uint32_t)i) * 0x9E3779B9u + tile;
+      e[reg][7] &= 0x3fffffffu;
+      return;
+    }
     const rg_u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
     const rg_u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16u, 0, 0);
     e[reg][0] = v0.x; e[reg][1] = v0.y; e[reg][2] = v0.z; e[reg][3] = v0.w;
@@ -282,6 +291,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
     rg_u32x4 v0, v1;
     v0.x = e[reg][0]; v0.y = e[reg][1]; v0.z = e[reg][2]; v0.w = e[reg][3];
     v1.x = e[reg][4]; v1.y = e[reg][5]; v1.z = e[reg][6]; v1.w = e[reg][7];
+    if constexpr (PROBE != 0) {  // canonical values never have a top word of ~0
+      if (v1.w != ~0u) return;
+    }
     __builtin_amdgcn_raw_buffer_store_b128(v0, rout, off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v1, rout, off + 16u, 0, 0);
   };

@@ -813,7 +813,7 @@ static rg_status launch_r2_pf(const NttArgs<L>& a, hipStream_t st) {
 static inline bool r2_prefetch_enabled() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("RINGO_NTT_PREFETCH");
+    const char* e = knob(Knob::NttPrefetch);
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
@@ -1048,7 +1048,7 @@ static rg_status launch_r8_pf(const NttArgs<1>& a, hipStream_t st) {
   if (!cap) {  // persistent grid: the resident capacity (RINGO_NTT_WG_PER_CU overrides)
     int per_cu = 0, dev = 0, cus = 256;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>, 512, 0);
-    const char* e = getenv("RINGO_NTT_WG_PER_CU");
+    const char* e = knob(Knob::NttWgPerCu);
     if (e) per_cu = atoi(e);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1061,7 +1061,7 @@ static rg_status launch_r8_pf(const NttArgs<1>& a, hipStream_t st) {
 
 template <bool INV, bool SCALE, bool COL, bool QLO1>
 static rg_status launch_r8_q(const NttArgs<1>& a, hipStream_t st) {
-  static const int pf = getenv("RINGO_NTT_R8_PF") ? atoi(getenv("RINGO_NTT_R8_PF")) : 0;
+  static const int pf = knob(Knob::NttR8Pf) ? atoi(knob(Knob::NttR8Pf)) : 0;
   return pf ? launch_r8_pf<INV, SCALE, COL, QLO1, true>(a, st)
                                : launch_r8_pf<INV, SCALE, COL, QLO1, false>(a, st);
 }
@@ -1075,7 +1075,7 @@ static rg_status launch_r8(const NttArgs<1>& a, hipStream_t st) {
 static inline bool use_r8() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("RINGO_NTT_KERNEL");
+    const char* e = knob(Knob::NttKernel);
     v = (e && e[0] == 'r' && e[1] == '2') ? 0 : 1;
   }
   return v == 1;
@@ -1092,7 +1092,7 @@ static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
   // chunk the batch so the pass-to-pass intermediate stays in the 256 MiB Infinity Cache
   static size_t chunk_bytes = 0;
   if (!chunk_bytes) {  // RINGO_NTT_CHUNK_MB overrides the Infinity-Cache-sized chunk (tuning)
-    const char* e = getenv("RINGO_NTT_CHUNK_MB");
+    const char* e = knob(Knob::NttChunkMb);
     chunk_bytes = (size_t)(e ? atoi(e) : 192) << 20;
   }
   size_t chunk = std::max<size_t>(1, chunk_bytes / (poly_u64 * 8));

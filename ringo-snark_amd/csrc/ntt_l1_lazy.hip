@@ -1,9 +1,8 @@
 // ntt_l1_lazy.hip -- dispatch of the lazy single-word pass kernels (ntt64.hpp) for the shapes
 // they cover: N = 2^16 as two 8-stage passes, q < 2^63 with q mod 2^32 == 1 (the config-2
 // jindo-modulus prime 47104^4 + 1 and every other p - 1 = b^(2^e) with b even).  Other shapes
-// keep the generic kernels of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r8|r2 forces the generic path.
-#include <cstdlib>
-
+// keep the generic kernels of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r8|r2 forces the generic path
+// (experiments build only, common.hpp).
 #include "ntt64.hpp"
 #include "ntt_plan.hpp"
 
@@ -12,7 +11,7 @@ namespace rg {
 static bool lazy_disabled() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("RINGO_NTT_KERNEL");
+    const char* e = knob(Knob::NttKernel);
     v = (e && e[0] == 'r') ? 1 : 0;
   }
   return v == 1;
@@ -23,7 +22,7 @@ static bool lazy_disabled() {
 template <bool INV, bool COL, bool SCALE, bool CANON>
 static rg_status launch64(const Ntt64Args& a, size_t polys, hipStream_t st) {
   const long long tiles = a.total_sub / 16;
-  if (measure_probe() == 4) {  // bench.py's compute-floor measurement (rg_set_probe): no HBM data movement
+  if (measure_probe() == 4) {  // bench.py's compute floor (rg_set_probe, experiments build): no HBM data movement
     if (!COL && polys % 16 == 0)
       hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, true, 1, 4>), dim3((unsigned)tiles), dim3(512), 0, st, a);
     else
@@ -56,7 +55,7 @@ rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled) {
   a.logN = p.logN;
   static size_t chunk_polys = 0;
   if (!chunk_polys) {  // RINGO_NTT_CHUNK_MB bounds the polys per pass pair (default: whole batch)
-    const char* e = getenv("RINGO_NTT_CHUNK_MB");
+    const char* e = knob(Knob::NttChunkMb);
     chunk_polys = e ? std::max<size_t>(1, ((size_t)atoi(e) << 20) / (N * 8)) : ~(size_t)0 >> 1;
   }
   for (size_t b0 = 0; b0 < p.batch; b0 += chunk_polys) {

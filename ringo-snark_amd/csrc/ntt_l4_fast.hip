@@ -1,8 +1,7 @@
 // ntt_l4_fast.hip -- dispatch of the 4-limb degree-2^16 / 2^15 kernels (ntt256.hpp) for q = 1 mod 2^64,
 // q < 2^255 (the Jindo default prime q255).  Other 4-limb shapes keep the generic CIOS kernels
-// of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r... forces the generic path (A/B switch).
-#include <cstdlib>
-
+// of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r... forces the generic path (A/B switch; experiments
+// build only, common.hpp).
 #include "ntt256.hpp"
 #include "ntt_plan.hpp"
 
@@ -11,6 +10,13 @@ namespace rg {
 template <bool INV, bool COL, bool SCALE, bool CANON, int LOGN>
 static rg_status launch256(const Ntt256Args& a, size_t polys, hipStream_t st) {
   const unsigned grid = (unsigned)(polys << (LOGN - 10));  // 1024 points (32 KiB) per workgroup
+  if (LOGN == 16 && measure_probe() == 5) {  // bench.py's L = 4 compute floor (experiments build)
+    if (!COL && polys % 4 == 0)
+      hipLaunchKernelGGL((ntt256_pass<INV, COL, SCALE, CANON, true, LOGN, 1>), dim3(grid), dim3(128), 0, st, a);
+    else
+      hipLaunchKernelGGL((ntt256_pass<INV, COL, SCALE, CANON, false, LOGN, 1>), dim3(grid), dim3(128), 0, st, a);
+    return check_launch("ntt256_pass (probe)");
+  }
   if (!COL && polys % 4 == 0)
     hipLaunchKernelGGL((ntt256_pass<INV, COL, SCALE, CANON, true, LOGN>), dim3(grid), dim3(128), 0, st, a);
   else
@@ -38,7 +44,7 @@ rg_status ntt256_run(const NttLaunch& p, hipStream_t st, bool* handled) {
   if (p.npasses != 2 || p.passes[1].P != 8 || !((p.logN == 16 && p.passes[0].P == 8) || (p.logN == 15 && p.passes[0].P == 7)))
     return RG_OK;
   if (p.q[0] != 1 || (p.q[3] >> 63) != 0) return RG_OK;
-  const char* e = getenv("RINGO_NTT_KERNEL");
+  const char* e = knob(Knob::NttKernel);
   if (e && e[0] == 'r') return RG_OK;
   *handled = true;
   const size_t N = (size_t)1 << p.logN;

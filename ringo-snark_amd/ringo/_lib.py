@@ -5,7 +5,10 @@ import os
 import re
 
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("RINGO_LIB") or os.path.join(_ROOT, "lib", "libringo.so")  # RINGO_LIB: profiling variants
+# RINGO_LIB: another build of the same ABI (tools/: profiling variants, the experiments build)
+LIB_PATH = os.environ.get("RINGO_LIB") or os.path.join(_ROOT, "lib", "libringo.so")
+# the experiments build (ringo-snark_amd/Makefile): RINGO_* kernel switches and rg_set_probe honoured
+EXP_LIB_PATH = os.path.join(_ROOT, "lib", "libringo_exp.so")
 HEADER = os.path.join(os.path.dirname(_ROOT), "include", "ringo.h")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -108,6 +111,7 @@ _SIGS = {
                                            vp]),
     "rg_jindo_scratch_bytes": (ctypes.c_size_t, [vp, ctypes.c_size_t]),
     "rg_jindo_release_stream": (ctypes.c_int, [vp, vp]),
+    "rg_jindo_mac_kinds": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "rg_jindo_eval_batch_dev": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "rg_jindo_eval_partial_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "rg_jindo_eval_reduce_dev": (ctypes.c_int, [vp, vp, vp, vp, vp]),
@@ -134,6 +138,24 @@ def header_symbols():
     return sorted(set(re.findall(r"\b(rg_[a-z0-9_]+)\s*\(", src)) - {"rg_status"})
 
 
+def load(path):
+    """A libringo build at `path` with every ABI signature set (a second, independent copy when
+    `path` differs from the loaded product library: bench.py loads the experiments build this way
+    for its compute-floor legs)."""
+    try:
+        import torch  # noqa: F401  (see lib())
+    except ImportError:
+        pass
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built: run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -148,12 +170,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libringo.so not built at {LIB_PATH}: run __graft_entry__.build() "
                                "(there is no CPU fallback for the product path)")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
 
 

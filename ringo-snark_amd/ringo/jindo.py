@@ -245,6 +245,14 @@ class Prover:
                                                 _addr(enc, _words(sh["enc"])), _addr(mlwe, _words(sh["mlwe_out"])),
                                                 _addr(com, _words(sh["com"])), _stream(stream)))
 
+    MAC_KINDS = {0: "generic", 1: "valu3", 2: "mfma"}  # include/ringo.h RG_MAC_*
+
+    def mac_kinds(self):
+        """(inner, outer): which kernel runs each Ajtai product of this handle."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(lib().rg_jindo_mac_kinds(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return self.MAC_KINDS[a.value], self.MAC_KINDS[b.value]
+
     def release_stream(self, stream=None):
         """Drop the scratch the handle caches for `stream` (rg_jindo_release_stream)."""
         check(lib().rg_jindo_release_stream(self.h, _stream(stream)))

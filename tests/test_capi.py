@@ -73,3 +73,41 @@ def test_null_handles_rejected_no_gpu():
     assert L.rg_jindo_commit(None, None, 0, None, None, None, None, None, None, None, None) == -1
     h = ctypes.c_void_p()
     assert L.rg_field_create(1, _lib.ptr(np.array([4], np.uint64)), ctypes.byref(h)) == -1  # even modulus
+
+
+def test_production_library_refuses_probe_no_gpu():
+    """libringo.so has no measurement switch: rg_set_probe refuses every probe but 0, and no
+    source of the product reads the environment (the RINGO_* kernel switches live only in the
+    experiments build, tools/experiments/knobs_env.hip)."""
+    L = _lib.lib()
+    for probe in (1, 4, 5, -1):
+        assert L.rg_set_probe(probe) == -1  # RG_ERR_INVALID
+    assert L.rg_set_probe(0) == 0
+    import glob
+    import os
+    csrc = os.path.join(os.path.dirname(_lib._ROOT), "ringo-snark_amd", "csrc")
+    for fn in glob.glob(os.path.join(csrc, "*")):
+        assert "getenv" not in open(fn).read(), fn
+
+
+def test_experiments_library_honours_probe_no_gpu():
+    """libringo_exp.so: the same ABI, probes 4 and 5 accepted (per calling thread), others not."""
+    import threading
+    E = _lib.load(_lib.EXP_LIB_PATH)
+    assert E.rg_set_probe(4) == 0
+    assert E.rg_set_probe(5) == 0
+    assert E.rg_set_probe(3) == -1
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(E.rg_set_probe(0)))
+    t.start()
+    t.join()
+    assert seen == [0]
+    assert E.rg_set_probe(0) == 0
+    for n in _lib.header_symbols():
+        assert hasattr(E, n), n
+
+
+def test_mac_kinds_argument_errors_no_gpu():
+    L = _lib.lib()
+    a, b = ctypes.c_int(), ctypes.c_int()
+    assert L.rg_jindo_mac_kinds(None, ctypes.byref(a), ctypes.byref(b)) == -1

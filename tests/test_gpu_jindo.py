@@ -235,23 +235,40 @@ def test_evaluate_batch_shards_sum_to_whole():
 
 
 
-@pytest.mark.parametrize("name,nv", [("t14_b1", 16384), ("mult_t8193_b12", 8193), ("t10_b8", 1024)])
-def test_mac_paths_agree(name, nv, monkeypatch):
+MAC_SHAPES = [("t14_b1", 16384), ("mult_t8193_b12", 8193), ("t10_b8", 1024)]
+
+
+def test_mac_paths_agree(tmp_path):
     """The three inner/outer MAC kernels (the MFMA digit MAC, mac3h on the VALU, mac_kernel)
-    produce the same Opening.InCommit and Commitment.Value bit for bit; RINGO_JINDO_MAC is read
-    when a prover's commit key is installed."""
-    P, q, params = _setup(name)
-    v = make_v(q, nv, seed=5)
-    rnd = make_randomness(P, q, seed=9)
-    outs = {}
-    for mode in ("", "h", "l"):
-        if mode:
-            monkeypatch.setenv("RINGO_JINDO_MAC", mode)
-        else:
-            monkeypatch.delenv("RINGO_JINDO_MAC", raising=False)
+    produce the same Opening.InCommit and Commitment.Value bit for bit.  The product library
+    (this process) must run the MFMA MAC on both products of every shape; the other two run in
+    child processes on the experiments build with RINGO_JINDO_MAC=h / l (tests/exp_child.py), each
+    checked to have taken the kernel it names.  MSIS ranks J > 16 (examples/mult's 21) take
+    mac_kernel in every mode: there this compares the product's fallback with itself, and
+    test_commit_matches_oracle pins it."""
+    import subprocess
+    import sys
+
+    def expect(J, mode):
+        if J > 16 or mode == "l":
+            return "generic"
+        return "valu3" if mode == "h" else "mfma"
+
+    want = {}
+    for name, nv in MAC_SHAPES:
+        P, q, params = _setup(name)
         prv = jindo.NewProver(params, b"Jindo!")
-        com, op = prv.Commit(v, jindo.Randomness(**rnd))
-        outs[mode] = (op.InCommit.copy(), com.Value.copy())
+        assert prv.mac_kinds() == (expect(P["in_msis"], ""), expect(P["out_msis"], "")), name
+        com, op = prv.Commit(make_v(q, nv, seed=5), jindo.Randomness(**make_randomness(P, q, seed=9)))
+        want[name] = (op.InCommit.copy(), com.Value.copy())
     for mode in ("h", "l"):
-        assert (outs[""][0] == outs[mode][0]).all(), (name, mode, "InCommit")
-        assert (outs[""][1] == outs[mode][1]).all(), (name, mode, "Commitment")
+        out = tmp_path / f"mac_{mode}.npz"
+        r = subprocess.run([sys.executable, os.path.join(HERE, "exp_child.py"), "mac", mode, str(out)] +
+                           [f"{n}:{nv}" for n, nv in MAC_SHAPES], capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got = np.load(out)
+        for name, _ in MAC_SHAPES:
+            P = PARAMS[name]
+            assert tuple(got[name + "/kinds"]) == (expect(P["in_msis"], mode), expect(P["out_msis"], mode)), (name, mode)
+            assert (got[name + "/incom"] == want[name][0]).all(), (name, mode, "InCommit")
+            assert (got[name + "/com"] == want[name][1]).all(), (name, mode, "Commitment")

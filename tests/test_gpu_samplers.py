@@ -293,3 +293,24 @@ def test_commit_sampled_concurrent_streams():
     jobs[0]["st"].synchronize()
     for k in keys:
         assert torch.equal(again[k], jobs[0]["out"][k]), k
+
+
+def test_unsupported_sampling_shape_refused():
+    """Device sampling covers d = 256, slots % 4 == 0 and encode TwinCDT tables of <= 96 entries
+    (every NewParameters shape of a field with exp <= 64).  Outside that the sampled entry points
+    return RG_ERR_UNSUPPORTED with the reason, before any launch: here an encode stddev far above
+    NewParameters' ecdStdDev (a 2,000-entry table)."""
+    import torch
+    from ringo._lib import RingoError
+    P = PARAMS["t10_b1"]
+    q = int(P["field_q_hex"], 16)
+    params = jindo.Parameters.from_dict(P, q)
+    sd = list(params.stddevs)
+    sd[0] = 400.0
+    params.stddevs = tuple(sd)
+    prv = jindo.NewProver(params, b"Jindo!")
+    v = make_v(q, 64, seed=5)[None]
+    sh = params.shapes(1)
+    o = {k: torch.zeros(sh[k], dtype=torch.int64, device="cuda") for k in ("last_row", "mask", "enc_noise", "mlwe_noise")}
+    with pytest.raises(RingoError, match="TwinCDT table"):
+        prv.sample_dev(1, _t(v), 64, _seeds(b"big"), 0, o["last_row"], o["mask"], o["enc_noise"], o["mlwe_noise"])
