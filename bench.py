@@ -87,7 +87,8 @@ def parse():
     ap.add_argument("--logn", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the L=4 / Jindo lines")
-    ap.add_argument("--extra", default="l4,j14,j16", help="secondary lines to run: l4, j14, j16 (comma list)")
+    ap.add_argument("--extra", default="l4,wide,j14,j16",
+                    help="secondary lines to run: l4, wide, j14, j16 (comma list)")
     ap.add_argument("--no-ntt", action="store_true", help="skip the headline NTT line (profiling one line)")
     ap.add_argument("--no-prewarm", action="store_true", help="no time-based prewarm (deterministic step count)")
     ap.add_argument("--plumbing", action="store_true",
@@ -173,7 +174,7 @@ def ntt_step_bench(torch, ringo, dist, q, L, batch, logn, steps, warmup, seed):
     ok = bool(torch.equal(x, ref))  # fwd then inv is the identity: full-size self-check
     kern_ms = ev.total_ms()
     floor_ms = None
-    if logn == 16:
+    if logn == 16 and L in (1, 4):
         floor_ms = compute_floor(torch, ringo, q, L, N, batch, x, stream, steps, warmup)
         ok = ok and bool(torch.equal(x, ref))
     return dict(wall_s=wall, kernel_ms=kern_ms, ok=ok, ntts=2 * batch * steps, N=N, L=L, compute_floor_ms=floor_ms)
@@ -754,6 +755,20 @@ def main():
                          "pointwise_mul": {"unit": "elements/s", "value": world * vm["elems_per_s"],
                                            "achieved_GBs": vm["achieved_GBs"], "elements": 64 * N},
                          "bigpoly_ops": polyops_bench(torch, ringo, Q255, 4, N, 64, 10, 13 + rank)}
+    if "wide" in extra:
+        fields = json.load(open(os.path.join(ROOT, "tests", "golden", "fields.json")))
+        for fname, bw in (("zp440", 32), ("zp880", 16)):
+            qw = int(fields[fname]["q_hex"], 16)
+            Lw = (qw.bit_length() + 63) // 64
+            stw = max(2, args.steps // 4)
+            rw = ntt_step_bench(torch, ringo, dist, qw, Lw, bw, args.logn, stw, 1, 17 + rank)
+            msw, kw = reduce_max(torch, dist, rw["wall_s"] * 1000.0 / stw, rw["kernel_ms"])
+            out["wide_ntt_" + fname] = {
+                "value": world * 2 * bw / (msw / 1000.0), "unit": "NTT/s",
+                "config": f"Buckler wide field {fname} ({qw.bit_length()}-bit, L={Lw}): fwd+inv negacyclic NTT, "
+                          f"N=2^{args.logn}, batch {bw}/GPU (buckler_test.go:163-222 runs zp880 at LogN 15)",
+                "achieved_GBs": 2 * N * 8 * Lw * rw["ntts"] / (kw / 1000.0) / 1e9,
+                "ms_per_step": msw, "selfcheck_fwd_inv_identity": rw["ok"]}
     for cfg, jb, key in (("t14_b1", args.j14_batch, "j14"), ("t16_b4096", args.j16_batch, "j16")):
         if key not in extra:
             continue
