@@ -19,7 +19,7 @@ void set_last_error(const std::string& msg);
 // (tools/experiments/knobs_env.hip), reads them from the RINGO_* environment and honours
 // rg_set_probe; the production library has no environment access at all.
 enum class Knob : int {
-  NttKernel,   // RINGO_NTT_KERNEL   r2 | r8 | r*: generic single-word / q255 pass kernels
+  NttKernel,   // RINGO_NTT_KERNEL   r2 | r8 | r*: generic single-word / q255 pass kernels; stage: wide fields per stage
   NttChunkMb,  // RINGO_NTT_CHUNK_MB polys per pass pair bounded to this many MiB
   NttPrefetch, // RINGO_NTT_PREFETCH 0: no next-tile register prefetch in ntt_r2
   NttWgPerCu,  // RINGO_NTT_WG_PER_CU persistent ntt_r8 grid size

@@ -634,6 +634,10 @@ __global__ __launch_bounds__(256) void mac_kernel(MacArgs a, int j0) {
     const uint64_t* A = (set ? a.A2 : a.A1) + lk;
     const uint64_t* Bp = (set ? a.B2 : a.B1) + lk;
     const long long bcol = set ? a.b2_col : a.b1_col, bterm = set ? a.b2_term : a.b1_term;
+    // J = 1 (Prover.Evaluate's dot products): unrolled so each thread keeps 4 terms' loads in
+    // flight -- one term's 1 + NC loads per iteration left the opening stream latency-bound
+    constexpr int kUnr = JB == 1 ? 4 : 1;
+#pragma unroll kUnr
     for (int t = 0; t < T; ++t) {
       uint64_t av[JB], bv[NC];
 #pragma unroll

@@ -1,0 +1,230 @@
+// ntt_wide.hpp -- LDS-tiled pass kernel for the wide Buckler fields (zp440: L = 7, zp880: L = 14
+// 64-bit limbs), the NTT math/bigpoly/ntt.go:98-136,206-244 runs for buckler_test.go:163-222.
+//
+// Cost model.  A 14-limb Montgomery product is ~3,100 half-rate VALU operations, so at these
+// widths the transform is bound by the multiplier, not by HBM: a 2^16-point zp880 transform is
+// ~0.5 G wave-lane multiplies against 7.3 MB of data.  What the one-launch-per-stage kernel
+// (ntt_stage_kernel) wasted was 16 HBM round trips per transform plus a 64-bit-limb CIOS with
+// explicit compare-based carries.  Here:
+//   * passes of P <= 8 stages (N = 2^16: COL 8 + ROW 8, N = 2^15: 7 + 8, N <= 2^8: one pass):
+//     a workgroup loads `cpt` sub-transforms (2^P points at stride S) into limb-planar LDS, runs
+//     the P radix-2 stages with one butterfly per thread per step and a barrier between stages,
+//     and writes the tile back -- HBM sees one read and one write per element per pass;
+//   * the product is Montgomery on 32-bit digits (D = 2L), product scanning with a 96-bit column
+//     accumulator: one v_mad_u64_u32 with carry-out plus one v_addc per partial product, the
+//     quotient digit m_k = t_k (-q^-1) mod 2^32 per column: 2 D^2 products, no compares;
+//   * every value stays canonical in [0, q) (one conditional subtract per add / sub / product:
+//     ~3 D operations against ~4 D^2 for the product), so limbs equal the reference's.
+// Twiddles are the reference's Montgomery tables tw[m + i] / twInv[m + i], read from L2; the
+// inverse's N^-1 is fused into global stage 0 as in the other kernels ((u+v) N^-1,
+// (u-v) twInv[1] N^-1).  Requires q < 2^(64L - 1) (checked by the launcher), so a Montgomery
+// product of canonical inputs is < 2q < 2^(64L).
+#pragma once
+#include <stdint.h>
+
+#include "ntt64.hpp"
+
+namespace rg {
+
+constexpr int kWideThreads = 128;  // threads per workgroup
+constexpr int kWideMaxL = 14;
+
+struct WideArgs {
+  const uint64_t* in;
+  uint64_t* out;
+  const uint64_t* tw;  // Montgomery [N][L]
+  uint32_t q[2 * kWideMaxL];
+  uint32_t nsc[2 * kWideMaxL];  // N^-1, Montgomery
+  uint32_t w1n[2 * kWideMaxL];  // twInv[1] N^-1, Montgomery
+  uint32_t qinv32;              // -q^-1 mod 2^32
+  int logN, G0, P, logS, cpt;   // pass: global stages [G0, G0 + P), points at stride 2^logS
+  long long nsub;               // sub-transforms of the pass over the batch
+  int scale;                    // inverse pass holding global stage 0: fuse N^-1
+};
+
+#if defined(__HIPCC__)
+
+// z = x y 2^(-32 D) mod q, canonical, for canonical x, y and q < 2^(32 D - 1)
+template <int D>
+__device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
+                                          const uint32_t (&q)[D], uint32_t qi) {
+  uint32_t m[D];
+  uint64_t A = 0;
+  uint32_t H = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * D - 1; ++k) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int j = k - i;
+      if (j < 0 || j >= D) continue;
+      lmask c, c2;
+      A = mad_co(x[i], y[j], A, c);
+      H = addc_co(H, 0u, c, c2);
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int j = k - i;
+      if (i >= k || j < 1 || j >= D) continue;
+      lmask c, c2;
+      A = mad_co(m[i], q[j], A, c);
+      H = addc_co(H, 0u, c, c2);
+    }
+    if (k < D) {  // quotient digit: clears the column's low word
+      m[k] = lo32(A) * qi;
+      lmask c, c2;
+      A = mad_co(m[k], q[0], A, c);
+      H = addc_co(H, 0u, c, c2);
+    } else {
+      z[k - D] = lo32(A);
+    }
+    A = pk(hi32(A), H);
+    H = 0;
+  }
+  z[D - 1] = lo32(A);
+  // [0, 2q) -> [0, q)
+  uint32_t u[D];
+  lmask b;
+  u[0] = sub_co(z[0], q[0], b);
+#pragma unroll
+  for (int i = 1; i < D; ++i) u[i] = subb_co(z[i], q[i], b, b);
+#pragma unroll
+  for (int i = 0; i < D; ++i) z[i] = sel(b, z[i], u[i]);
+}
+
+template <int D>
+__device__ __forceinline__ void add_wide(uint32_t (&r)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
+                                         const uint32_t (&q)[D]) {
+  uint32_t s[D], u[D];
+  lmask c, b;
+  s[0] = add_co(x[0], y[0], c);
+#pragma unroll
+  for (int i = 1; i < D; ++i) s[i] = addc_co(x[i], y[i], c, c);
+  u[0] = sub_co(s[0], q[0], b);
+#pragma unroll
+  for (int i = 1; i < D; ++i) u[i] = subb_co(s[i], q[i], b, b);
+  const lmask m = c | ~b;
+#pragma unroll
+  for (int i = 0; i < D; ++i) r[i] = sel(m, u[i], s[i]);
+}
+
+template <int D>
+__device__ __forceinline__ void sub_wide(uint32_t (&r)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
+                                         const uint32_t (&q)[D]) {
+  uint32_t d[D], f[D];
+  lmask b, c;
+  d[0] = sub_co(x[0], y[0], b);
+#pragma unroll
+  for (int i = 1; i < D; ++i) d[i] = subb_co(x[i], y[i], b, b);
+  f[0] = add_co(d[0], q[0], c);
+#pragma unroll
+  for (int i = 1; i < D; ++i) f[i] = addc_co(d[i], q[i], c, c);
+#pragma unroll
+  for (int i = 0; i < D; ++i) r[i] = sel(b, f[i], d[i]);
+}
+
+// One pass over `cpt` sub-transforms per workgroup.  LDS: limb planes of u64, plane l holds
+// element (c, x) at c 2^P + x.  Stages are a runtime loop (the body is one butterfly), so P, the
+// strides and the pass position are arguments, not template parameters.
+template <int L, bool INV>
+__global__ __launch_bounds__(kWideThreads) void ntt_wide_pass(WideArgs a) {
+  constexpr int D = 2 * L;
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const int P = a.P, NP = 1 << P, cpt = a.cpt, logS = a.logS;
+  const int plane = cpt * NP;
+  const long long s0 = (long long)blockIdx.x * cpt;
+  const int subs_log = a.logN - P;  // log2 sub-transforms per polynomial
+  uint32_t q[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) q[i] = a.q[i];
+  const uint32_t qi = a.qinv32;
+  // global element index of point x of tile sub-transform c (or -1 past the batch)
+  auto elem = [&](int c, int x) -> long long {
+    const long long s = s0 + c;
+    if (s >= a.nsub) return -1;
+    const long long b = s >> subs_log, r = s & ((1LL << subs_log) - 1);
+    const long long hi = r >> logS, lo = r & ((1LL << logS) - 1);
+    return (b << a.logN) | (hi << (a.logN - a.G0)) | ((long long)x << logS) | lo;
+  };
+  // ---- HBM -> LDS: memory-friendly order (rows: c, x, l; columns: x, c, l)
+  const int W = cpt * NP * L;
+  for (int f = threadIdx.x; f < W; f += kWideThreads) {
+    const int l = f % L, e = f / L;
+    const int c = logS == 0 ? e / NP : e % cpt, x = logS == 0 ? e % NP : e / cpt;
+    const long long g = elem(c, x);
+    if (g >= 0) lds[l * plane + c * NP + x] = a.in[g * L + l];
+  }
+  __syncthreads();
+  // ---- the P stages
+  const int nbf = cpt * (NP >> 1);
+  for (int st = 0; st < P; ++st) {
+    const int g = INV ? P - 1 - st : st;  // local stage (global G0 + g)
+    const int bitpos = P - 1 - g;
+    const bool last = INV && a.scale && (a.G0 + g == 0);
+    for (int bf = threadIdx.x; bf < nbf; bf += kWideThreads) {
+      const int c = bf >> (P - 1), p = bf & ((NP >> 1) - 1);
+      const int x0 = ((p >> bitpos) << (bitpos + 1)) | (p & ((1 << bitpos) - 1)), x1 = x0 | (1 << bitpos);
+      const long long s = s0 + c;
+      const long long r = s & ((1LL << subs_log) - 1);
+      const long long hi = (r >> logS) & ((1LL << a.G0) - 1);
+      uint32_t u[D], v[D], w[D];
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        const uint64_t uu = lds[l * plane + c * NP + x0], vv = lds[l * plane + c * NP + x1];
+        u[2 * l] = lo32(uu);
+        u[2 * l + 1] = hi32(uu);
+        v[2 * l] = lo32(vv);
+        v[2 * l + 1] = hi32(vv);
+      }
+      if (last) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) w[i] = a.w1n[i];
+      } else {
+        const long long idx = (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
+        const uint64_t* tp = a.tw + idx * L;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          const uint64_t t = tp[l];
+          w[2 * l] = lo32(t);
+          w[2 * l + 1] = hi32(t);
+        }
+      }
+      uint32_t nu[D], nv[D];
+      if constexpr (!INV) {  // ntt.go:254-259
+        uint32_t t[D];
+        mont_wide<D>(t, v, w, q, qi);
+        add_wide<D>(nu, u, t, q);
+        sub_wide<D>(nv, u, t, q);
+      } else {  // ntt.go:365-370 (+ 242-243 at global stage 0)
+        uint32_t d[D];
+        sub_wide<D>(d, u, v, q);
+        add_wide<D>(nu, u, v, q);
+        mont_wide<D>(nv, d, w, q, qi);
+        if (last) {
+          uint32_t ns[D], t[D];
+#pragma unroll
+          for (int i = 0; i < D; ++i) ns[i] = a.nsc[i];
+          mont_wide<D>(t, nu, ns, q, qi);
+#pragma unroll
+          for (int i = 0; i < D; ++i) nu[i] = t[i];
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        lds[l * plane + c * NP + x0] = pk(nu[2 * l], nu[2 * l + 1]);
+        lds[l * plane + c * NP + x1] = pk(nv[2 * l], nv[2 * l + 1]);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- LDS -> HBM
+  for (int f = threadIdx.x; f < W; f += kWideThreads) {
+    const int l = f % L, e = f / L;
+    const int c = logS == 0 ? e / NP : e % cpt, x = logS == 0 ? e % NP : e / cpt;
+    const long long g = elem(c, x);
+    if (g >= 0) a.out[g * L + l] = lds[l * plane + c * NP + x];
+  }
+}
+
+#endif  // __HIPCC__
+
+}  // namespace rg

@@ -2,7 +2,8 @@
 
 Mirrors what the reference exercises through bigpoly (math/bigpoly/ntt.go, vec.go,
 base_op.go): every generated field of the reference, cyclic and negacyclic transformers,
-ranks from 8 to 2^16 (2^14 for the wide fields), batched, aliasing out == in."""
+ranks from 2 to 2^16 (the wide fields through ntt_wide_pass up to Buckler's 2^15 / 2^16),
+batched, aliasing out == in."""
 import numpy as np
 import pytest
 
@@ -18,8 +19,8 @@ CASES = [  # (field, logN list)
     ("mult_zp", [4, 10]),
     ("zp220", [5, 9, 14]),
     ("bfv_zp", [8]),
-    ("zp440", [3, 8, 10]),
-    ("zp880", [3, 6, 9]),
+    ("zp440", [1, 3, 8, 10, 11, 15, 16]),
+    ("zp880", [2, 6, 9, 13, 15, 16]),
 ]
 
 
