@@ -53,6 +53,11 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
   uint32_t H = 0;
 #pragma unroll
   for (int k = 0; k < 2 * D - 1; ++k) {
+    // two independent carry chains per column (x y products into A/H, m q products into B/G),
+    // merged once per column: a single chain of dependent v_mad_u64_u32 leaves the SIMD idle at
+    // the 2 waves/SIMD the 14-limb registers allow
+    uint64_t B = 0;
+    uint32_t G = 0;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       const int j = k - i;
@@ -66,8 +71,15 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
       const int j = k - i;
       if (i >= k || j < 1 || j >= D) continue;
       lmask c, c2;
-      A = mad_co(m[i], q[j], A, c);
-      H = addc_co(H, 0u, c, c2);
+      B = mad_co(m[i], q[j], B, c);
+      G = addc_co(G, 0u, c, c2);
+    }
+    if (k > 0) {  // A/H += B/G
+      lmask c, c2, c3;
+      const uint32_t lo = add_co(lo32(A), lo32(B), c);
+      const uint32_t hi = addc_co(hi32(A), hi32(B), c, c2);
+      A = pk(lo, hi);
+      H = addc_co(H, G, c2, c3);
     }
     if (k < D) {  // quotient digit: clears the column's low word
       m[k] = lo32(A) * qi;
