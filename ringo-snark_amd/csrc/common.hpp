@@ -28,6 +28,7 @@ enum class Knob : int {
   JindoPrepW,  // RINGO_JINDO_PREP_W minimum waves/SIMD of prep256 (1, 6, 8)
   JindoMac,    // RINGO_JINDO_MAC    h: mac3h, l: mac_kernel instead of the MFMA MAC
   JindoSplit,  // RINGO_JINDO_SPLIT  0: commit_sampled on the caller's stream only
+  JindoEval,   // RINGO_JINDO_EVAL   mac: Evaluate's batch combination on mac_kernel, not dot_split_kernel
   Count
 };
 const char* knob(Knob k);

@@ -2775,6 +2775,71 @@ static MacArgs dot_args(const RnsPrime* P, int nl, int d, long long nout, int T,
   return m;
 }
 
+// Prover.Evaluate's batch combination (prover.go:254-266): a J = 1 dot product over the batch's
+// T commits, out[col][lk] = (sum_t A[t][lk] B[col][t][lk]) 2^-64 mod q, read once from HBM.
+// T = batch is the long axis (512 at the configs[4] shard) and the column count is modest (the
+// 144 InCommit / 432 MLWE polynomials), so mac_kernel's thread per (4 columns, lk) left too few
+// waves in flight for the opening stream.  Here a 256-thread workgroup owns 64 lk x NC columns
+// and its 4 waves split the terms (wave w: t = w, w + 4, ...), each term's loads unrolled x2;
+// the four exact 128-bit partial sums are added through LDS, then reduced once.
+constexpr int kDotNC = 4;
+__global__ __launch_bounds__(256) void dot_split_kernel(MacArgs a) {
+  __shared__ uint64_t red[3][kDotNC][2][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long per_col = (long long)a.nl * a.d;
+  const long long nlkb = per_col / 64;
+  const long long lk = (blockIdx.x % nlkb) * 64 + lane;
+  const long long col0 = (blockIdx.x / nlkb) * kDotNC;
+  const int nc = (int)min((long long)kDotNC, a.ncols - col0);
+  const int T = a.T1;
+  Acc<false> acc[kDotNC];
+#pragma unroll
+  for (int c = 0; c < kDotNC; ++c) acc[c].zero();
+  const uint64_t* A = a.A1 + lk;
+  const uint64_t* Bp = a.B1 + lk;
+#pragma unroll 2
+  for (int t = w; t < T; t += 4) {
+    const uint64_t av = A[(long long)t * per_col];
+    uint64_t bv[kDotNC];
+#pragma unroll
+    for (int c = 0; c < kDotNC; ++c) bv[c] = c < nc ? Bp[(col0 + c) * a.b1_col + t * a.b1_term] : 0;
+#pragma unroll
+    for (int c = 0; c < kDotNC; ++c) acc[c].mac(av, bv[c]);
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int c = 0; c < kDotNC; ++c) {
+      red[w - 1][c][0][lane] = acc[c].lo;
+      red[w - 1][c][1][lane] = acc[c].hi;
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const RnsPrime& P = a.P[(int)(lk / a.d)];
+#pragma unroll
+  for (int c = 0; c < kDotNC; ++c) {
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {  // exact: (lo, hi) += (lo', hi'), the sum stays below 2^128
+      uint32_t cy = 0;
+      acc[c].lo = addc(acc[c].lo, red[v][c][0][lane], cy);
+      acc[c].hi += red[v][c][1][lane] + cy;
+    }
+    if (c < nc) a.out[(col0 + c) * per_col + lk] = acc[c].reduce(P);
+  }
+}
+
+static rg_status launch_dot(const MacArgs& m, hipStream_t st) {
+  uint64_t qmax = 0;
+  for (int l = 0; l < m.nl; ++l) qmax = std::max(qmax, m.P[l].q);
+  const bool narrow = 2.0 * log2((double)(qmax - 1)) + log2((double)m.T1 + 1.0) < 127.5;
+  const char* k = knob(Knob::JindoEval);  // experiments build: RINGO_JINDO_EVAL=mac (A/B)
+  if (m.J != 1 || m.T2 != 0 || m.C || !narrow || (m.nl * m.d) % 64 != 0 || (k && k[0] == 'm'))
+    return launch_mac(m, st);
+  const long long blocks = (m.ncols + kDotNC - 1) / kDotNC * ((long long)m.nl * m.d / 64);
+  hipLaunchKernelGGL(dot_split_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+  return check_launch("jindo eval dot");
+}
+
 static rg_status eval_batch(const rg_jindo* J, size_t batch, const uint64_t* incom, const uint64_t* enc,
                             const uint64_t* mlwe, const uint64_t* bq, const uint64_t* bo, uint64_t* ob_incom,
                             uint64_t* ob_enc, uint64_t* ob_mlwe, hipStream_t st) {
@@ -2788,9 +2853,9 @@ static rg_status eval_batch(const rg_jindo* J, size_t batch, const uint64_t* inc
     return RG_OK;
   }
   const int T = (int)batch;  // term i = commit i, scaled by its batch challenge (:254-266)
-  RG_TRY(launch_mac(dot_args(J->ro, p.nqo, p.d, n_inc, T, bo, incom, po, n_inc * po, ob_incom), st));
-  RG_TRY(launch_mac(dot_args(J->rq, p.nq, p.d, n_enc, T, bq, enc, pq, n_enc * pq, ob_enc), st));
-  RG_TRY(launch_mac(dot_args(J->rq, p.nq, p.d, n_ml, T, bq, mlwe, pq, n_ml * pq, ob_mlwe), st));
+  RG_TRY(launch_dot(dot_args(J->ro, p.nqo, p.d, n_inc, T, bo, incom, po, n_inc * po, ob_incom), st));
+  RG_TRY(launch_dot(dot_args(J->rq, p.nq, p.d, n_enc, T, bq, enc, pq, n_enc * pq, ob_enc), st));
+  RG_TRY(launch_dot(dot_args(J->rq, p.nq, p.d, n_ml, T, bq, mlwe, pq, n_ml * pq, ob_mlwe), st));
   return RG_OK;
 }
 
