@@ -22,6 +22,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #include "ntt64.hpp"
 
 namespace rg {
@@ -44,6 +47,28 @@ struct WideArgs {
 
 #if defined(__HIPCC__)
 
+// Compile-time loops: the 14-limb product is ~1,600 partial products, past what the loop unroller
+// fully unrolls, and a rolled loop indexes the digit arrays dynamically (s_set_gpr_idx, measured
+// 5x slower than the per-stage kernel).  static_for expands every index at compile time.
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// (H, A) += x y as ONE asm statement: hipcc pads one wait state after an asm statement before a
+// VALU that reads its outputs, so a separate mad and carry add cost a pad each; paired here and
+// with the two chains' statements alternating, every output is first read two statements later.
+__device__ __forceinline__ void mac_wide(uint64_t& A, uint32_t& H, uint32_t x, uint32_t y) {
+  lmask c;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32 %1, %2, %1, 0, %2"
+      : "+v"(A), "+v"(H), "=&s"(c)
+      : "v"(x), "v"(y));
+}
+
 // z = x y 2^(-32 D) mod q, canonical, for canonical x, y and q < 2^(32 D - 1)
 template <int D>
 __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
@@ -51,37 +76,30 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
   uint32_t m[D];
   uint64_t A = 0;
   uint32_t H = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * D - 1; ++k) {
+  static_for<2 * D - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     // two independent carry chains per column (x y products into A/H, m q products into B/G),
-    // merged once per column: a single chain of dependent v_mad_u64_u32 leaves the SIMD idle at
-    // the 2 waves/SIMD the 14-limb registers allow
+    // interleaved in program order and merged once per column: one chain of dependent
+    // v_mad_u64_u32 leaves the SIMD idle at the 2 waves/SIMD the wide registers allow
+    constexpr int xlo = k < D ? 0 : k - D + 1, xhi = k < D ? k : D - 1;          // x y: i in [xlo, xhi]
+    constexpr int mlo = k < D ? 0 : k - D + 1, mhi = k < D ? k - 1 : D - 1;      // m q: i in [mlo, mhi], j >= 1
+    constexpr int nx = xhi - xlo + 1, nm = mhi >= mlo ? mhi - mlo + 1 : 0;
+    constexpr int nmax = nx > nm ? nx : nm;
     uint64_t B = 0;
     uint32_t G = 0;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int j = k - i;
-      if (j < 0 || j >= D) continue;
-      lmask c, c2;
-      A = mad_co(x[i], y[j], A, c);
-      H = addc_co(H, 0u, c, c2);
-    }
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int j = k - i;
-      if (i >= k || j < 1 || j >= D) continue;
-      lmask c, c2;
-      B = mad_co(m[i], q[j], B, c);
-      G = addc_co(G, 0u, c, c2);
-    }
-    if (k > 0) {  // A/H += B/G
+    static_for<nmax>([&](auto ic) {
+      constexpr int r = decltype(ic)::value;
+      if constexpr (r < nx) mac_wide(A, H, x[xlo + r], y[k - xlo - r]);
+      if constexpr (r < nm) mac_wide(B, G, m[mlo + r], q[k - mlo - r]);
+    });
+    if constexpr (nm > 0) {  // A/H += B/G
       lmask c, c2, c3;
       const uint32_t lo = add_co(lo32(A), lo32(B), c);
       const uint32_t hi = addc_co(hi32(A), hi32(B), c, c2);
       A = pk(lo, hi);
       H = addc_co(H, G, c2, c3);
     }
-    if (k < D) {  // quotient digit: clears the column's low word
+    if constexpr (k < D) {  // quotient digit: clears the column's low word
       m[k] = lo32(A) * qi;
       lmask c, c2;
       A = mad_co(m[k], q[0], A, c);
@@ -91,7 +109,7 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
     }
     A = pk(hi32(A), H);
     H = 0;
-  }
+  });
   z[D - 1] = lo32(A);
   // [0, 2q) -> [0, q)
   uint32_t u[D];
@@ -138,7 +156,7 @@ __device__ __forceinline__ void sub_wide(uint32_t (&r)[D], const uint32_t (&x)[D
 // element (c, x) at c 2^P + x.  Stages are a runtime loop (the body is one butterfly), so P, the
 // strides and the pass position are arguments, not template parameters.
 template <int L, bool INV>
-__global__ __launch_bounds__(kWideThreads) void ntt_wide_pass(WideArgs a) {
+__global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  // >= 2 waves/SIMD (<= 256 VGPRs)
   constexpr int D = 2 * L;
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const int P = a.P, NP = 1 << P, cpt = a.cpt, logS = a.logS;
@@ -210,14 +228,21 @@ __global__ __launch_bounds__(kWideThreads) void ntt_wide_pass(WideArgs a) {
         uint32_t d[D];
         sub_wide<D>(d, u, v, q);
         add_wide<D>(nu, u, v, q);
-        mont_wide<D>(nv, d, w, q, qi);
-        if (last) {
-          uint32_t ns[D], t[D];
+        // one product site (the I-cache holds one expanded 14-limb product, not two): the last
+        // stage runs it a second time for (u + v) N^-1
+        for (int rep = 0; rep < (last ? 2 : 1); ++rep) {
+          uint32_t in[D], f[D], t[D];
 #pragma unroll
-          for (int i = 0; i < D; ++i) ns[i] = a.nsc[i];
-          mont_wide<D>(t, nu, ns, q, qi);
+          for (int i = 0; i < D; ++i) {
+            in[i] = rep ? nu[i] : d[i];
+            f[i] = rep ? a.nsc[i] : w[i];
+          }
+          mont_wide<D>(t, in, f, q, qi);
 #pragma unroll
-          for (int i = 0; i < D; ++i) nu[i] = t[i];
+          for (int i = 0; i < D; ++i) {
+            if (rep) nu[i] = t[i];
+            else nv[i] = t[i];
+          }
         }
       }
 #pragma unroll
