@@ -38,7 +38,7 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
     G0s[1] = logN / 2;
     Ps[1] = logN - logN / 2;
   }
-  const int base_cpt = L <= 7 ? 2 : 1;
+  const int base_cpt = 1;  // one 256-point sub-transform per workgroup at P = 8: 14 / 28 KiB of LDS, so LDS does not cap occupancy below the VGPRs
   for (int k = 0; k < np; ++k) {
     const int i = p.inv ? np - 1 - k : k;
     a.G0 = G0s[i];
