@@ -41,14 +41,10 @@ typedef int mfma_v4i __attribute__((ext_vector_type(4)));
 #ifndef RG_MFMA_STAGES
 #define RG_MFMA_STAGES 4
 #endif
-#ifndef RG_MFMA_CT
-#define RG_MFMA_CT 1  // 8-term chunks per ring stage (one barrier per stage)
-#endif
 #ifndef RG_MFMA_LK
 #define RG_MFMA_LK 16  // lk per workgroup: 16 (1024 threads, one 128-B line) or 8 (512 threads, 2 per CU: measured 30% slower)
 #endif
 constexpr int kMfmaStages = RG_MFMA_STAGES;  // LDS ring depth
-constexpr int kMfmaCt = RG_MFMA_CT;
 
 __device__ __forceinline__ void mfma_glds16(const void* gsrc, uint32_t lds_dst) {
   uint32_t keep;
@@ -74,8 +70,7 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
   constexpr int ND = 2 * NB - 1;      // diagonals
   constexpr int NP = LK / 2;          // lk pairs
   constexpr int BW = 8 * NP * 16 * 2;  // opening words per stage
-  constexpr int CW = BW + LK * 128;    // words per 8-term chunk (opening, then the waves' key chunks)
-  constexpr int SW = kMfmaCt * CW;     // stage words
+  constexpr int SW = BW + LK * 128;    // stage words
   static_assert(16 * 16 * LK <= kMfmaStages * SW, "output stage must fit the ring");
   __shared__ uint64_t ring[kMfmaStages * SW];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -92,21 +87,16 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
   const long long dc = std::min<long long>(c0 + dcol, a.ncols - 1);
   // the wave's key chunk (1 KiB of [lk][chunk][64 lanes][2]): the lane's own 16 B
   const uint64_t* akey = a.Ak + (lk0 + w) * Tc * 128 + 2 * lane;
-  // stage `sc` (chunks kMfmaCt sc ..): 2 LDS-DMAs per wave and chunk (16 B of opening, 16 B of key
-  // per lane); past the last chunk they reload valid addresses into a free stage, so every
-  // iteration issues the same count
-  auto stage = [&](int sc) {
-#pragma unroll
-    for (int u = 0; u < kMfmaCt; ++u) {
-      const int chunk = sc * kMfmaCt + u;
-      int t = chunk * 8 + dt;
-      if (t >= T) t = T - 1;  // the key's padded terms are zero
-      const uint64_t* src = t < a.T1 ? a.B1 + dc * a.b1_col + (long long)t * a.b1_term
-                                     : a.B2 + dc * a.b2_col + (long long)(t - a.T1) * a.b2_term;
-      const uint32_t base = ring_lds + (uint32_t)((sc % kMfmaStages) * SW + u * CW) * 8u;
-      mfma_glds16(src + lk0 + 2 * dp, base + (uint32_t)(w * 128) * 8u);
-      mfma_glds16(akey + (long long)std::min(chunk, Tc - 1) * 128, base + (uint32_t)(BW + w * 128) * 8u);
-    }
+  // stage `chunk`: 2 LDS-DMAs per wave (16 B of opening, 16 B of key per lane); past the last
+  // chunk they reload valid addresses into a free stage, so every iteration issues the same count
+  auto stage = [&](int chunk) {
+    int t = chunk * 8 + dt;
+    if (t >= T) t = T - 1;  // the key's padded terms are zero
+    const uint64_t* src = t < a.T1 ? a.B1 + dc * a.b1_col + (long long)t * a.b1_term
+                                   : a.B2 + dc * a.b2_col + (long long)(t - a.T1) * a.b2_term;
+    const uint32_t base = ring_lds + (uint32_t)((chunk % kMfmaStages) * SW) * 8u;
+    mfma_glds16(src + lk0 + 2 * dp, base + (uint32_t)(w * 128) * 8u);
+    mfma_glds16(akey + (long long)std::min(chunk, Tc - 1) * 128, base + (uint32_t)(BW + w * 128) * 8u);
   };
   mfma_v4i acc[ND];
 #pragma unroll
@@ -116,34 +106,29 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
   // LDS words of the lane's two opening values: terms 2 (lane >> 4) + {0, 1}, lk = lk0 + w
   // (pair w >> 1, half w & 1), column lane & 15
   const int rd = ((2 * (lane >> 4) * NP + (w >> 1)) * 16 + (lane & 15)) * 2 + (w & 1);
-  const int Ts = (Tc + kMfmaCt - 1) / kMfmaCt;  // stages
-  for (int c = 0; c < Ts; ++c) {
-    mfma_wait_vm<2 * kMfmaCt * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
-    __builtin_amdgcn_s_barrier();                      // ... for every wave; stage c - 1 is free
+  for (int c = 0; c < Tc; ++c) {
+    mfma_wait_vm<2 * (kMfmaStages - 2)>();  // stage c landed (stages c+1 .. c+S-2 may be in flight)
+    __builtin_amdgcn_s_barrier();           // ... for every wave; stage c - 1 is free
     stage(c + kMfmaStages - 1);
+    const uint64_t* st = ring + (c % kMfmaStages) * SW;
+    const uint64_t b0 = st[rd] ^ a.bxor, b1 = st[rd + NP * 32] ^ a.bxor;  // + NP 32 words: term + 1
+    const ulonglong2 ak = *reinterpret_cast<const ulonglong2*>(st + BW + w * 128 + 2 * lane);
+    mfma_v4i bv;
+    bv[0] = (int)(uint32_t)b0;
+    bv[1] = (int)(uint32_t)(b0 >> 32);
+    bv[2] = (int)(uint32_t)b1;
+    bv[3] = (int)(uint32_t)(b1 >> 32);
 #pragma unroll
-    for (int u = 0; u < kMfmaCt; ++u) {
-      if (kMfmaCt > 1 && c * kMfmaCt + u >= Tc) break;  // the last stage's padding chunk (uniform)
-      const uint64_t* st = ring + (c % kMfmaStages) * SW + u * CW;
-      const uint64_t b0 = st[rd] ^ a.bxor, b1 = st[rd + NP * 32] ^ a.bxor;  // + NP 32 words: term + 1
-      const ulonglong2 ak = *reinterpret_cast<const ulonglong2*>(st + BW + w * 128 + 2 * lane);
-      mfma_v4i bv;
-      bv[0] = (int)(uint32_t)b0;
-      bv[1] = (int)(uint32_t)(b0 >> 32);
-      bv[2] = (int)(uint32_t)b1;
-      bv[3] = (int)(uint32_t)(b1 >> 32);
-#pragma unroll
-      for (int s = 0; s < ND; ++s) {
-        const int sh = NB - 1 - s;  // A operand of diagonal s: byte b = digit s - b
-        const uint64_t x0 = sh >= 0 ? ak.x >> (8 * sh) : ak.x << (-8 * sh);
-        const uint64_t x1 = sh >= 0 ? ak.y >> (8 * sh) : ak.y << (-8 * sh);
-        mfma_v4i av;
-        av[0] = (int)(uint32_t)x0;
-        av[1] = (int)(uint32_t)(x0 >> 32);
-        av[2] = (int)(uint32_t)x1;
-        av[3] = (int)(uint32_t)(x1 >> 32);
-        acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[s], 0, 0, 0);
-      }
+    for (int s = 0; s < ND; ++s) {
+      const int sh = NB - 1 - s;  // A operand of diagonal s: byte b = digit s - b
+      const uint64_t x0 = sh >= 0 ? ak.x >> (8 * sh) : ak.x << (-8 * sh);
+      const uint64_t x1 = sh >= 0 ? ak.y >> (8 * sh) : ak.y << (-8 * sh);
+      mfma_v4i av;
+      av[0] = (int)(uint32_t)x0;
+      av[1] = (int)(uint32_t)(x0 >> 32);
+      av[2] = (int)(uint32_t)x1;
+      av[3] = (int)(uint32_t)(x1 >> 32);
+      acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[s], 0, 0, 0);
     }
   }
   mfma_wait_vm<0>();

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the RG_MFMA_CT / RG_MFMA_KEYREG variants exist only with tools/experiments/mac_mfma_stage_keyreg.patch applied)
 # Round 4 MFMA MAC A/B: chunks per ring stage (RG_MFMA_CT) x ring depth (RG_MFMA_STAGES), each
 # variant checked for correctness (NB = 5 / 6 / 8, odd chunk counts) and timed at the configs[4]
 # inner-MAC half batch (T 545, J 16, 2304 columns) and the configs[2] one.  Binaries are built
