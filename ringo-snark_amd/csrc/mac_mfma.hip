@@ -41,9 +41,6 @@ typedef int mfma_v4i __attribute__((ext_vector_type(4)));
 #ifndef RG_MFMA_STAGES
 #define RG_MFMA_STAGES 4
 #endif
-#ifndef RG_MFMA_SGB
-#define RG_MFMA_SGB 1  // interleave each diagonal's MFMA with the VALU that forms the next A operand
-#endif
 #ifndef RG_MFMA_LK
 #define RG_MFMA_LK 16  // lk per workgroup: 16 (1024 threads, one 128-B line) or 8 (512 threads, 2 per CU: measured 30% slower)
 #endif
@@ -90,24 +87,15 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
   const long long dc = std::min<long long>(c0 + dcol, a.ncols - 1);
   // the wave's key chunk (1 KiB of [lk][chunk][64 lanes][2]): the lane's own 16 B
   const uint64_t* akey = a.Ak + (lk0 + w) * Tc * 128 + 2 * lane;
-  // the lane's opening rows of both term sets, and both term strides held in registers: with a
-  // select on the kernel argument itself, hipcc re-read the stride from the argument segment every
-  // chunk (an s_load and an lgkmcnt(0) wait on the chunk's critical path)
-  const uint64_t* base1 = a.B1 + dc * a.b1_col + lk0 + 2 * dp;
-  const uint64_t* base2 = a.B2 + dc * a.b2_col + lk0 + 2 * dp;
-  const uint32_t st1lo = __builtin_amdgcn_readfirstlane((uint32_t)a.b1_term), st1hi = __builtin_amdgcn_readfirstlane((uint32_t)(a.b1_term >> 32));
-  const uint32_t st2lo = __builtin_amdgcn_readfirstlane((uint32_t)a.b2_term), st2hi = __builtin_amdgcn_readfirstlane((uint32_t)(a.b2_term >> 32));
-  const long long st1 = (long long)(((uint64_t)st1hi << 32) | st1lo), st2 = (long long)(((uint64_t)st2hi << 32) | st2lo);
   // stage `chunk`: 2 LDS-DMAs per wave (16 B of opening, 16 B of key per lane); past the last
   // chunk they reload valid addresses into a free stage, so every iteration issues the same count
   auto stage = [&](int chunk) {
     int t = chunk * 8 + dt;
     if (t >= T) t = T - 1;  // the key's padded terms are zero
-    const uint64_t* s1 = base1 + (long long)t * st1;
-    const uint64_t* s2 = base2 + (long long)(t - a.T1) * st2;
-    const uint64_t* src = t < a.T1 ? s1 : s2;
+    const uint64_t* src = t < a.T1 ? a.B1 + dc * a.b1_col + (long long)t * a.b1_term
+                                   : a.B2 + dc * a.b2_col + (long long)(t - a.T1) * a.b2_term;
     const uint32_t base = ring_lds + (uint32_t)((chunk % kMfmaStages) * SW) * 8u;
-    mfma_glds16(src, base + (uint32_t)(w * 128) * 8u);
+    mfma_glds16(src + lk0 + 2 * dp, base + (uint32_t)(w * 128) * 8u);
     mfma_glds16(akey + (long long)std::min(chunk, Tc - 1) * 128, base + (uint32_t)(BW + w * 128) * 8u);
   };
   mfma_v4i acc[ND];
@@ -142,17 +130,6 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
       av[3] = (int)(uint32_t)(x1 >> 32);
       acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[s], 0, 0, 0);
     }
-#if RG_MFMA_SGB
-    // hipcc emits all of the chunk's shifts first and the MFMAs as one burst; with the 4 waves of a
-    // SIMD in lockstep (one barrier per chunk) the VALU and matrix pipes then take turns.  Ask for
-    // the A operands to be formed one diagonal ahead of each MFMA instead.
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS_READ: the chunk's opening and key reads first
-#pragma unroll
-    for (int s = 0; s < ND; ++s) {
-      __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);  // VALU: the next diagonal's shifted key words
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // MFMA
-    }
-#endif
   }
   mfma_wait_vm<0>();
   __syncthreads();

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (mmc_sgb0 / mmc_sgb1 are built from tools/experiments/mac_mfma_sched_interleave.patch applied)
 # Round 4 MFMA MAC A/B: the round-3 kernel (mmc_base) vs the term strides pinned in registers with
 # hipcc's MFMA burst left alone (mmc_sgb0) or interleaved with the VALU that forms the next A
 # operand (mmc_sgb1, sched_group_barrier); correctness, then configs[4] / configs[2] timings.
