@@ -183,6 +183,39 @@ __device__ __forceinline__ uint32_t divstep_b2(uint32_t r, uint32_t n0, uint32_t
   return qt;
 }
 
+// x R^-1 mod q for a canonical x (Slice = fromMont, element.go): Montgomery reduction alone, L^2
+// word products instead of the 2 L^2 of f_mul(x, 1).  The result is canonical: (x + m q) / R < q + 1,
+// and equals q only when x = 0, which gives m = 0 and 0.
+template <int L>
+__device__ __forceinline__ void f_redc(uint64_t* z, const uint64_t* x, const FieldParams<L>& F) {
+  uint64_t t[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) t[i] = x[i];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const uint64_t m = t[0] * F.qinv;
+    uint64_t lo, hi;
+    mul_wide(m, F.q[0], lo, hi);
+    uint32_t c0 = 0;
+    addc(lo, t[0], c0);  // == 0 mod 2^64; only the carry is kept
+    uint64_t carry = hi + c0;
+#pragma unroll
+    for (int j = 1; j < L; ++j) {
+      mul_wide(m, F.q[j], lo, hi);
+      uint32_t c = 0;
+      lo = addc(lo, t[j], c);
+      hi += c;
+      c = 0;
+      lo = addc(lo, carry, c);
+      t[j - 1] = lo;
+      carry = hi + c;
+    }
+    t[L - 1] = carry;
+  }
+#pragma unroll
+  for (int i = 0; i < L; ++i) z[i] = t[i];
+}
+
 template <int L>
 __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
   const JShape& S = a.s;
@@ -230,10 +263,8 @@ __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
     for (int l = 0; l < L; ++l) x[l] = have ? vb[i * L + l] : 0;
   }
   // canonical limbs (Slice = fromMont)
-  uint64_t one[L], c[L];
-#pragma unroll
-  for (int l = 0; l < L; ++l) one[l] = (l == 0);
-  f_mul<L>(c, x, one, a.F);
+  uint64_t c[L];
+  f_redc<L>(c, x, a.F);
   if (!have) {
 #pragma unroll
     for (int l = 0; l < L; ++l) c[l] = 0;
