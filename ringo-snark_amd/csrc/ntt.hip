@@ -192,6 +192,25 @@ static rg_status finalize(rg_ntt* t) {
     t->nsc_sh = h_shoup(nv, q);
     t->w1n[0] = wv;
     t->w1n_sh = h_shoup(wv, q);
+  } else if (L == 7 || L == 14) {
+    // wide fields: the inverse table is followed by twInv[i] / 2 (ntt_wide.hpp's inverse halves
+    // every stage instead of scaling by N^-1 at the end); the per-stage kernels read the first half
+    RG_TRY(t->d_tw.upload(t->h_tw.data(), t->h_tw.size() * 8));
+    std::vector<uint64_t> b(2 * t->h_twinv.size());
+    const size_t half = t->h_twinv.size();
+    memcpy(b.data(), t->h_twinv.data(), half * 8);
+    for (int i = 0; i < N; ++i) {
+      const uint64_t* x = &t->h_twinv[(size_t)i * L];
+      uint64_t* z = &b[half + (size_t)i * L];
+      uint64_t c = 0;
+      if (x[0] & 1) c = HostField::add_n(z, x, t->f.q, L);
+      else memcpy(z, x, 8 * L);
+      for (int l = 0; l < L; ++l) z[l] = (z[l] >> 1) | ((l + 1 < L ? z[l + 1] : c) << 63);
+    }
+    RG_TRY(t->d_twinv.upload(b.data(), b.size() * 8));
+    memcpy(t->nsc, &t->h_ninv[0], 8 * L);
+    memcpy(t->w1n, w1n, 8 * L);
+    t->nsc_sh = t->w1n_sh = 0;
   } else {
     RG_TRY(t->d_tw.upload(t->h_tw.data(), t->h_tw.size() * 8));
     RG_TRY(t->d_twinv.upload(t->h_twinv.data(), t->h_twinv.size() * 8));

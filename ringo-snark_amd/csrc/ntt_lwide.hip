@@ -14,14 +14,11 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
   if (logN < 1 || logN > 16 || !spare || (k && k[0] == 's')) return run_stages<L, false>(p, st);
   WideArgs a;
   memset(&a, 0, sizeof(a));
-  a.tw = p.tw;
+  // inverse: the halved copy of twInv that ntt.hip's finalize() appends to the table
+  a.tw = p.inv ? p.tw + ((size_t)1 << logN) * L : p.tw;
   for (int l = 0; l < L; ++l) {
     a.q[2 * l] = (uint32_t)p.q[l];
     a.q[2 * l + 1] = (uint32_t)(p.q[l] >> 32);
-    a.nsc[2 * l] = (uint32_t)p.nsc[l];
-    a.nsc[2 * l + 1] = (uint32_t)(p.nsc[l] >> 32);
-    a.w1n[2 * l] = (uint32_t)p.w1n[l];
-    a.w1n[2 * l + 1] = (uint32_t)(p.w1n[l] >> 32);
   }
   a.qinv32 = (uint32_t)p.qinv;  // -q^-1 mod 2^64, so its low word is -q^-1 mod 2^32
   a.logN = logN;
@@ -47,7 +44,6 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
     a.cpt = std::max(base_cpt, 256 >> a.P);
     if (a.logS > 0) a.cpt = std::min(a.cpt, 1 << a.logS);  // a COL tile stays inside one row of columns
     a.nsub = (long long)p.batch << (logN - a.P);
-    a.scale = p.inv && a.G0 == 0;
     a.in = k == 0 ? p.in : p.out;
     a.out = p.out;
     const size_t lds = (size_t)a.cpt * ((size_t)1 << a.P) * L * 8;

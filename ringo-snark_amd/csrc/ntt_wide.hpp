@@ -15,10 +15,13 @@
 //     quotient digit m_k = t_k (-q^-1) mod 2^32 per column: 2 D^2 products, no compares;
 //   * every value stays canonical in [0, q) (one conditional subtract per add / sub / product:
 //     ~3 D operations against ~4 D^2 for the product), so limbs equal the reference's.
-// Twiddles are the reference's Montgomery tables tw[m + i] / twInv[m + i], read from L2; the
-// inverse's N^-1 is fused into global stage 0 as in the other kernels ((u+v) N^-1,
-// (u-v) twInv[1] N^-1).  Requires q < 2^(64L - 1) (checked by the launcher), so a Montgomery
-// product of canonical inputs is < 2q < 2^(64L).
+// Twiddles are the reference's Montgomery tables tw[m + i] / twInv[m + i], read from L2.  The
+// inverse halves every stage ((u + v) / 2, (u - v) twInv[m + i] / 2 from a halved copy of the
+// table) instead of multiplying by N^-1 after the last one: log N halvings are N^-1, a halving is
+// ~3 D operations, and the butterfly keeps ONE product site (a second one for the N^-1 factor
+// doubled the I-cache footprint and pushed the 14-limb kernel past 256 VGPRs).  Requires
+// q < 2^(64L - 1) (checked by the launcher), so a Montgomery product of canonical inputs is
+// < 2q < 2^(64L).
 #pragma once
 #include <stdint.h>
 
@@ -35,14 +38,11 @@ constexpr int kWideMaxL = 14;
 struct WideArgs {
   const uint64_t* in;
   uint64_t* out;
-  const uint64_t* tw;  // Montgomery [N][L]
+  const uint64_t* tw;  // Montgomery [N][L]: tw (forward) or twInv / 2 (inverse)
   uint32_t q[2 * kWideMaxL];
-  uint32_t nsc[2 * kWideMaxL];  // N^-1, Montgomery
-  uint32_t w1n[2 * kWideMaxL];  // twInv[1] N^-1, Montgomery
-  uint32_t qinv32;              // -q^-1 mod 2^32
-  int logN, G0, P, logS, cpt;   // pass: global stages [G0, G0 + P), points at stride 2^logS
-  long long nsub;               // sub-transforms of the pass over the batch
-  int scale;                    // inverse pass holding global stage 0: fuse N^-1
+  uint32_t qinv32;             // -q^-1 mod 2^32
+  int logN, G0, P, logS, cpt;  // pass: global stages [G0, G0 + P), points at stride 2^logS
+  long long nsub;              // sub-transforms of the pass over the batch
 };
 
 #if defined(__HIPCC__)
@@ -152,6 +152,20 @@ __device__ __forceinline__ void sub_wide(uint32_t (&r)[D], const uint32_t (&x)[D
   for (int i = 0; i < D; ++i) r[i] = sel(b, f[i], d[i]);
 }
 
+// r = x / 2 mod q for canonical x: (x + (x odd ? q : 0)) >> 1, canonical (x + q < 2q < 2^(32 D))
+template <int D>
+__device__ __forceinline__ void half_wide(uint32_t (&r)[D], const uint32_t (&x)[D], const uint32_t (&q)[D]) {
+  const uint32_t odd = 0u - (x[0] & 1u);
+  uint32_t s[D];
+  lmask c;
+  s[0] = add_co(x[0], q[0] & odd, c);
+#pragma unroll
+  for (int i = 1; i < D; ++i) s[i] = addc_co(x[i], q[i] & odd, c, c);
+#pragma unroll
+  for (int i = 0; i + 1 < D; ++i) r[i] = __builtin_amdgcn_alignbit(s[i + 1], s[i], 1);
+  r[D - 1] = s[D - 1] >> 1;
+}
+
 // One pass over `cpt` sub-transforms per workgroup.  LDS: limb planes of u64, plane l holds
 // element (c, x) at c 2^P + x.  Stages are a runtime loop (the body is one butterfly), so P, the
 // strides and the pass position are arguments, not template parameters.
@@ -189,7 +203,6 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
   for (int st = 0; st < P; ++st) {
     const int g = INV ? P - 1 - st : st;  // local stage (global G0 + g)
     const int bitpos = P - 1 - g;
-    const bool last = INV && a.scale && (a.G0 + g == 0);
     for (int bf = threadIdx.x; bf < nbf; bf += kWideThreads) {
       const int c = bf >> (P - 1), p = bf & ((NP >> 1) - 1);
       const int x0 = ((p >> bitpos) << (bitpos + 1)) | (p & ((1 << bitpos) - 1)), x1 = x0 | (1 << bitpos);
@@ -205,10 +218,7 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         v[2 * l] = lo32(vv);
         v[2 * l + 1] = hi32(vv);
       }
-      if (last) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) w[i] = a.w1n[i];
-      } else {
+      auto load_w = [&]() {
         const long long idx = (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
         const uint64_t* tp = a.tw + idx * L;
 #pragma unroll
@@ -217,33 +227,24 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
           w[2 * l] = lo32(t);
           w[2 * l + 1] = hi32(t);
         }
-      }
+      };
       uint32_t nu[D], nv[D];
       if constexpr (!INV) {  // ntt.go:254-259
+        load_w();
         uint32_t t[D];
         mont_wide<D>(t, v, w, q, qi);
         add_wide<D>(nu, u, t, q);
         sub_wide<D>(nv, u, t, q);
-      } else {  // ntt.go:365-370 (+ 242-243 at global stage 0)
-        uint32_t d[D];
+      } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
+        uint32_t d[D], s[D];
         sub_wide<D>(d, u, v, q);
-        add_wide<D>(nu, u, v, q);
-        // one product site (the I-cache holds one expanded 14-limb product, not two): the last
-        // stage runs it a second time for (u + v) N^-1
-        for (int rep = 0; rep < (last ? 2 : 1); ++rep) {
-          uint32_t in[D], f[D], t[D];
-#pragma unroll
-          for (int i = 0; i < D; ++i) {
-            in[i] = rep ? nu[i] : d[i];
-            f[i] = rep ? a.nsc[i] : w[i];
-          }
-          mont_wide<D>(t, in, f, q, qi);
-#pragma unroll
-          for (int i = 0; i < D; ++i) {
-            if (rep) nu[i] = t[i];
-            else nv[i] = t[i];
-          }
-        }
+        add_wide<D>(s, u, v, q);
+        half_wide<D>(nu, s, q);
+        // u and v are dead here: the twiddle load is held behind the add / sub so the 14-limb
+        // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
+        __builtin_amdgcn_sched_barrier(0);
+        load_w();
+        mont_wide<D>(nv, d, w, q, qi);  // w = twInv / 2
       }
 #pragma unroll
       for (int l = 0; l < L; ++l) {
