@@ -237,9 +237,9 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         sub_wide<D>(nv, u, t, q);
       } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
         uint32_t d[D], s[D];
-        sub_wide<D>(d, u, v, q);
         add_wide<D>(s, u, v, q);
         half_wide<D>(nu, s, q);
+        sub_wide<D>(d, u, v, q);
         // u and v are dead here: the twiddle load is held behind the add / sub so the 14-limb
         // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
         __builtin_amdgcn_sched_barrier(0);
