@@ -69,6 +69,30 @@ __device__ __forceinline__ void mac_wide(uint64_t& A, uint32_t& H, uint32_t x, u
       : "v"(x), "v"(y));
 }
 
+// both chains' steps in ONE asm statement: the pad after a statement is then paid once per two
+// partial products
+__device__ __forceinline__ void mac_wide2(uint64_t& A, uint32_t& H, uint32_t x, uint32_t y, uint64_t& B,
+                                          uint32_t& G, uint32_t m, uint32_t n) {
+  lmask c, c2;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5"
+      : "+v"(A), "+v"(H), "+v"(B), "+v"(G), "=&s"(c), "=&s"(c2)
+      : "v"(x), "v"(y), "v"(m), "v"(n));
+}
+
+// two consecutive steps of both chains (four partial products) in one statement
+__device__ __forceinline__ void mac_wide4(uint64_t& A, uint32_t& H, uint32_t x0, uint32_t y0, uint32_t x1,
+                                          uint32_t y1, uint64_t& B, uint32_t& G, uint32_t m0, uint32_t n0,
+                                          uint32_t m1, uint32_t n1) {
+  lmask c, c2;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %10, %11, %2\n\t"
+      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5\n\t"
+      "v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %2, %5, %12, %13, %2\n\t"
+      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5"
+      : "+v"(A), "+v"(H), "+v"(B), "+v"(G), "=&s"(c), "=&s"(c2)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(m0), "v"(n0), "v"(m1), "v"(n1));
+}
+
 // z = x y 2^(-32 D) mod q, canonical, for canonical x, y and q < 2^(32 D - 1)
 template <int D>
 __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
@@ -89,8 +113,17 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
     uint32_t G = 0;
     static_for<nmax>([&](auto ic) {
       constexpr int r = decltype(ic)::value;
-      if constexpr (r < nx) mac_wide(A, H, x[xlo + r], y[k - xlo - r]);
-      if constexpr (r < nm) mac_wide(B, G, m[mlo + r], q[k - mlo - r]);
+      if constexpr (r % 2 == 1 && r < nx && r < nm) {
+        // paired into step r - 1's statement
+      } else if constexpr (r % 2 == 0 && r + 1 < nx && r + 1 < nm) {
+        mac_wide4(A, H, x[xlo + r], y[k - xlo - r], x[xlo + r + 1], y[k - xlo - r - 1], B, G, m[mlo + r],
+                  q[k - mlo - r], m[mlo + r + 1], q[k - mlo - r - 1]);
+      } else if constexpr (r < nx && r < nm) {
+        mac_wide2(A, H, x[xlo + r], y[k - xlo - r], B, G, m[mlo + r], q[k - mlo - r]);
+      } else {
+        if constexpr (r < nx) mac_wide(A, H, x[xlo + r], y[k - xlo - r]);
+        if constexpr (r < nm) mac_wide(B, G, m[mlo + r], q[k - mlo - r]);
+      }
     });
     if constexpr (nm > 0) {  // A/H += B/G
       lmask c, c2, c3;
@@ -209,15 +242,22 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
       const long long s = s0 + c;
       const long long r = s & ((1LL << subs_log) - 1);
       const long long hi = (r >> logS) & ((1LL << a.G0) - 1);
-      uint32_t u[D], v[D], w[D];
+      // the butterfly's operands come out of LDS when they are needed and its outputs go back as
+      // soon as they are final, so a 14-limb value is live only while it is used: the product's
+      // live set is its two inputs (+ u in the forward), and VGPRs, not LDS, set the occupancy
+      auto ld = [&](uint32_t(&r)[D], int x) {
 #pragma unroll
-      for (int l = 0; l < L; ++l) {
-        const uint64_t uu = lds[l * plane + c * NP + x0], vv = lds[l * plane + c * NP + x1];
-        u[2 * l] = lo32(uu);
-        u[2 * l + 1] = hi32(uu);
-        v[2 * l] = lo32(vv);
-        v[2 * l + 1] = hi32(vv);
-      }
+        for (int l = 0; l < L; ++l) {
+          const uint64_t t = lds[l * plane + c * NP + x];
+          r[2 * l] = lo32(t);
+          r[2 * l + 1] = hi32(t);
+        }
+      };
+      auto st = [&](const uint32_t(&r)[D], int x) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) lds[l * plane + c * NP + x] = pk(r[2 * l], r[2 * l + 1]);
+      };
+      uint32_t w[D];
       auto load_w = [&]() {
         const long long idx = (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
         const uint64_t* tp = a.tw + idx * L;
@@ -228,28 +268,32 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
           w[2 * l + 1] = hi32(t);
         }
       };
-      uint32_t nu[D], nv[D];
+      // sched_barrier: keeps the scheduler from hoisting a load above the point where the values
+      // it replaces die
       if constexpr (!INV) {  // ntt.go:254-259
+        uint32_t v[D], t[D];
         load_w();
-        uint32_t t[D];
+        ld(v, x1);
         mont_wide<D>(t, v, w, q, qi);
-        add_wide<D>(nu, u, t, q);
-        sub_wide<D>(nv, u, t, q);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t u[D], r[D];
+        ld(u, x0);
+        add_wide<D>(r, u, t, q);
+        st(r, x0);
+        sub_wide<D>(r, u, t, q);
+        st(r, x1);
       } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
-        uint32_t d[D], s[D];
-        add_wide<D>(s, u, v, q);
-        half_wide<D>(nu, s, q);
+        uint32_t u[D], v[D], r[D], d[D];
+        ld(u, x0);
+        ld(v, x1);
+        add_wide<D>(r, u, v, q);
+        half_wide<D>(d, r, q);
+        st(d, x0);
         sub_wide<D>(d, u, v, q);
-        // u and v are dead here: the twiddle load is held behind the add / sub so the 14-limb
-        // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
         __builtin_amdgcn_sched_barrier(0);
         load_w();
-        mont_wide<D>(nv, d, w, q, qi);  // w = twInv / 2
-      }
-#pragma unroll
-      for (int l = 0; l < L; ++l) {
-        lds[l * plane + c * NP + x0] = pk(nu[2 * l], nu[2 * l + 1]);
-        lds[l * plane + c * NP + x1] = pk(nv[2 * l], nv[2 * l + 1]);
+        mont_wide<D>(r, d, w, q, qi);  // w = twInv / 2
+        st(r, x1);
       }
     }
     __syncthreads();
