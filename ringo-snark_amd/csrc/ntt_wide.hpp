@@ -25,9 +25,7 @@
 #pragma once
 #include <stdint.h>
 
-#include <type_traits>
-#include <utility>
-
+#include "madc.hpp"
 #include "ntt64.hpp"
 
 namespace rg {
@@ -47,52 +45,6 @@ struct WideArgs {
 
 #if defined(__HIPCC__)
 
-// Compile-time loops: the 14-limb product is ~1,600 partial products, past what the loop unroller
-// fully unrolls, and a rolled loop indexes the digit arrays dynamically (s_set_gpr_idx, measured
-// 5x slower than the per-stage kernel).  static_for expands every index at compile time.
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// (H, A) += x y as ONE asm statement: hipcc pads one wait state after an asm statement before a
-// VALU that reads its outputs, so a separate mad and carry add cost a pad each; paired here and
-// with the two chains' statements alternating, every output is first read two statements later.
-__device__ __forceinline__ void mac_wide(uint64_t& A, uint32_t& H, uint32_t x, uint32_t y) {
-  lmask c;
-  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32 %1, %2, %1, 0, %2"
-      : "+v"(A), "+v"(H), "=&s"(c)
-      : "v"(x), "v"(y));
-}
-
-// both chains' steps in ONE asm statement: the pad after a statement is then paid once per two
-// partial products
-__device__ __forceinline__ void mac_wide2(uint64_t& A, uint32_t& H, uint32_t x, uint32_t y, uint64_t& B,
-                                          uint32_t& G, uint32_t m, uint32_t n) {
-  lmask c, c2;
-  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
-      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5"
-      : "+v"(A), "+v"(H), "+v"(B), "+v"(G), "=&s"(c), "=&s"(c2)
-      : "v"(x), "v"(y), "v"(m), "v"(n));
-}
-
-// two consecutive steps of both chains (four partial products) in one statement
-__device__ __forceinline__ void mac_wide4(uint64_t& A, uint32_t& H, uint32_t x0, uint32_t y0, uint32_t x1,
-                                          uint32_t y1, uint64_t& B, uint32_t& G, uint32_t m0, uint32_t n0,
-                                          uint32_t m1, uint32_t n1) {
-  lmask c, c2;
-  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %2, %5, %10, %11, %2\n\t"
-      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5\n\t"
-      "v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %2, %5, %12, %13, %2\n\t"
-      "v_addc_co_u32 %1, %4, %1, 0, %4\n\tv_addc_co_u32 %3, %5, %3, 0, %5"
-      : "+v"(A), "+v"(H), "+v"(B), "+v"(G), "=&s"(c), "=&s"(c2)
-      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(m0), "v"(n0), "v"(m1), "v"(n1));
-}
-
 // z = x y 2^(-32 D) mod q, canonical, for canonical x, y and q < 2^(32 D - 1)
 template <int D>
 __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
@@ -108,23 +60,12 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
     constexpr int xlo = k < D ? 0 : k - D + 1, xhi = k < D ? k : D - 1;          // x y: i in [xlo, xhi]
     constexpr int mlo = k < D ? 0 : k - D + 1, mhi = k < D ? k - 1 : D - 1;      // m q: i in [mlo, mhi], j >= 1
     constexpr int nx = xhi - xlo + 1, nm = mhi >= mlo ? mhi - mlo + 1 : 0;
-    constexpr int nmax = nx > nm ? nx : nm;
     uint64_t B = 0;
     uint32_t G = 0;
-    static_for<nmax>([&](auto ic) {
-      constexpr int r = decltype(ic)::value;
-      if constexpr (r % 2 == 1 && r < nx && r < nm) {
-        // paired into step r - 1's statement
-      } else if constexpr (r % 2 == 0 && r + 1 < nx && r + 1 < nm) {
-        mac_wide4(A, H, x[xlo + r], y[k - xlo - r], x[xlo + r + 1], y[k - xlo - r - 1], B, G, m[mlo + r],
-                  q[k - mlo - r], m[mlo + r + 1], q[k - mlo - r - 1]);
-      } else if constexpr (r < nx && r < nm) {
-        mac_wide2(A, H, x[xlo + r], y[k - xlo - r], B, G, m[mlo + r], q[k - mlo - r]);
-      } else {
-        if constexpr (r < nx) mac_wide(A, H, x[xlo + r], y[k - xlo - r]);
-        if constexpr (r < nm) mac_wide(B, G, m[mlo + r], q[k - mlo - r]);
-      }
-    });
+    madc_column<nx, nm>(
+        A, H, B, G, [&](auto r) { return x[xlo + decltype(r)::value]; },
+        [&](auto r) { return y[k - xlo - decltype(r)::value]; }, [&](auto r) { return m[mlo + decltype(r)::value]; },
+        [&](auto r) { return q[k - mlo - decltype(r)::value]; });
     if constexpr (nm > 0) {  // A/H += B/G
       lmask c, c2, c3;
       const uint32_t lo = add_co(lo32(A), lo32(B), c);
