@@ -183,22 +183,15 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
       const long long s = s0 + c;
       const long long r = s & ((1LL << subs_log) - 1);
       const long long hi = (r >> logS) & ((1LL << a.G0) - 1);
-      // the butterfly's operands come out of LDS when they are needed and its outputs go back as
-      // soon as they are final, so a 14-limb value is live only while it is used: the product's
-      // live set is its two inputs (+ u in the forward), and VGPRs, not LDS, set the occupancy
-      auto ld = [&](uint32_t(&r)[D], int x) {
+      uint32_t u[D], v[D], w[D];
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-          const uint64_t t = lds[l * plane + c * NP + x];
-          r[2 * l] = lo32(t);
-          r[2 * l + 1] = hi32(t);
-        }
-      };
-      auto st = [&](const uint32_t(&r)[D], int x) {
-#pragma unroll
-        for (int l = 0; l < L; ++l) lds[l * plane + c * NP + x] = pk(r[2 * l], r[2 * l + 1]);
-      };
-      uint32_t w[D];
+      for (int l = 0; l < L; ++l) {
+        const uint64_t uu = lds[l * plane + c * NP + x0], vv = lds[l * plane + c * NP + x1];
+        u[2 * l] = lo32(uu);
+        u[2 * l + 1] = hi32(uu);
+        v[2 * l] = lo32(vv);
+        v[2 * l + 1] = hi32(vv);
+      }
       auto load_w = [&]() {
         const long long idx = (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
         const uint64_t* tp = a.tw + idx * L;
@@ -209,32 +202,28 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
           w[2 * l + 1] = hi32(t);
         }
       };
-      // sched_barrier: keeps the scheduler from hoisting a load above the point where the values
-      // it replaces die
+      uint32_t nu[D], nv[D];
       if constexpr (!INV) {  // ntt.go:254-259
-        uint32_t v[D], t[D];
         load_w();
-        ld(v, x1);
+        uint32_t t[D];
         mont_wide<D>(t, v, w, q, qi);
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t u[D], r[D];
-        ld(u, x0);
-        add_wide<D>(r, u, t, q);
-        st(r, x0);
-        sub_wide<D>(r, u, t, q);
-        st(r, x1);
+        add_wide<D>(nu, u, t, q);
+        sub_wide<D>(nv, u, t, q);
       } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
-        uint32_t u[D], v[D], r[D], d[D];
-        ld(u, x0);
-        ld(v, x1);
-        add_wide<D>(r, u, v, q);
-        half_wide<D>(d, r, q);
-        st(d, x0);
+        uint32_t d[D], s[D];
+        add_wide<D>(s, u, v, q);
+        half_wide<D>(nu, s, q);
         sub_wide<D>(d, u, v, q);
+        // u and v are dead here: the twiddle load is held behind the add / sub so the 14-limb
+        // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
         __builtin_amdgcn_sched_barrier(0);
         load_w();
-        mont_wide<D>(r, d, w, q, qi);  // w = twInv / 2
-        st(r, x1);
+        mont_wide<D>(nv, d, w, q, qi);  // w = twInv / 2
+      }
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        lds[l * plane + c * NP + x0] = pk(nu[2 * l], nu[2 * l + 1]);
+        lds[l * plane + c * NP + x1] = pk(nv[2 * l], nv[2 * l + 1]);
       }
     }
     __syncthreads();
