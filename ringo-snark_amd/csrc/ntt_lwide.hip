@@ -21,6 +21,13 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
     a.q[2 * l + 1] = (uint32_t)(p.q[l] >> 32);
   }
   a.qinv32 = (uint32_t)p.qinv;  // -q^-1 mod 2^64, so its low word is -q^-1 mod 2^32
+  a.qinv28 = a.qinv32 & 0x0FFFFFFFu;
+  for (int k = 0; k < 64 * L / 28; ++k) {  // q in 28-bit digits
+    const int bit = 28 * k, l = bit >> 6, sh = bit & 63;
+    uint64_t v = p.q[l] >> sh;
+    if (sh > 36 && l + 1 < L) v |= p.q[l + 1] << (64 - sh);
+    a.q28[k] = (uint32_t)v & 0x0FFFFFFFu;
+  }
   a.logN = logN;
   // passes in forward order: (G0, P)
   int G0s[2], Ps[2], np;

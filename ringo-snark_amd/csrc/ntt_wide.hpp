@@ -39,6 +39,8 @@ struct WideArgs {
   const uint64_t* tw;  // Montgomery [N][L]: tw (forward) or twInv / 2 (inverse)
   uint32_t q[2 * kWideMaxL];
   uint32_t qinv32;             // -q^-1 mod 2^32
+  uint32_t q28[64 * kWideMaxL / 28];  // q in 28-bit digits (mont28)
+  uint32_t qinv28;                    // -q^-1 mod 2^28
   int logN, G0, P, logS, cpt;  // pass: global stages [G0, G0 + P), points at stride 2^logS
   long long nsub;              // sub-transforms of the pass over the batch
 };
@@ -85,6 +87,81 @@ __device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[
     H = 0;
   });
   z[D - 1] = lo32(A);
+  // [0, 2q) -> [0, q)
+  uint32_t u[D];
+  lmask b;
+  u[0] = sub_co(z[0], q[0], b);
+#pragma unroll
+  for (int i = 1; i < D; ++i) u[i] = subb_co(z[i], q[i], b, b);
+#pragma unroll
+  for (int i = 0; i < D; ++i) z[i] = sel(b, z[i], u[i]);
+}
+
+// The same product on 28-bit digits (K = 64 L / 28: 16 for L = 7, 32 for L = 14; R = 2^(28 K) =
+// 2^(64 L), so the result is the same Montgomery product).  A 28-bit digit product is < 2^56,
+// so a column of up to 2 K products plus the carry stays below 2^63 in one 64-bit accumulator:
+// no carry-out per partial product (the 32-bit-digit form pays a v_addc for each), and the
+// products are plain C that hipcc schedules and pads itself.  Digits are cut from and packed
+// back into the 32-bit words around the product (~2 operations per word each way).
+template <int L>
+__device__ __forceinline__ void to28(uint32_t (&d)[64 * L / 28], const uint32_t (&w)[2 * L]) {
+  constexpr int K = 64 * L / 28, D = 2 * L;
+  static_for<K>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int j = (28 * k) >> 5, sh = (28 * k) & 31;
+    if constexpr (sh <= 4 || j + 1 >= D)
+      d[k] = (w[j] >> sh) & 0x0FFFFFFFu;
+    else
+      d[k] = __builtin_amdgcn_alignbit(w[j + 1], w[j], sh) & 0x0FFFFFFFu;
+  });
+}
+template <int L>
+__device__ __forceinline__ void from28(uint32_t (&w)[2 * L], const uint32_t (&d)[64 * L / 28]) {
+  constexpr int K = 64 * L / 28, D = 2 * L;
+  static_for<D>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    constexpr int k0 = (32 * j) / 28, off = 32 * j - 28 * k0;  // word j starts at bit off of digit k0
+    uint32_t v = d[k0] >> off;
+    if constexpr (k0 + 1 < K) v |= d[k0 + 1] << (28 - off);
+    if constexpr (k0 + 2 < K && 56 - off < 32) v |= d[k0 + 2] << (56 - off);
+    w[j] = v;
+  });
+}
+template <int L>
+__device__ __forceinline__ void mont28(uint32_t (&z)[2 * L], const uint32_t (&x)[2 * L], const uint32_t (&y)[2 * L],
+                                       const uint32_t (&q)[2 * L], const uint32_t* q28, uint32_t qi28) {
+  constexpr int K = 64 * L / 28, D = 2 * L;
+  static_assert(64 * L % 28 == 0, "digit split");
+  uint32_t xd[K], yd[K], m[K], zd[K];
+  to28<L>(xd, x);
+  to28<L>(yd, y);
+  uint64_t C = 0;  // carry into the column: the previous column's sum >> 28
+  static_for<2 * K - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int xlo = k < K ? 0 : k - K + 1, xhi = k < K ? k : K - 1;
+    constexpr int mlo = k < K ? 0 : k - K + 1, mhi = k < K ? k - 1 : K - 1;  // m q, j = k - i >= 1
+    // two chains (x y, m q) for the SIMD's latency at 2 waves
+    uint64_t A = C, B = 0;
+    static_for<xhi - xlo + 1>([&](auto ic) {
+      constexpr int i = xlo + decltype(ic)::value;
+      A = (uint64_t)xd[i] * yd[k - i] + A;
+    });
+    if constexpr (mhi >= mlo)
+      static_for<mhi - mlo + 1>([&](auto ic) {
+        constexpr int i = mlo + decltype(ic)::value;
+        B = (uint64_t)m[i] * q28[k - i] + B;
+      });
+    uint64_t t = A + B;
+    if constexpr (k < K) {  // quotient digit: clears the column's 28 low bits
+      m[k] = ((uint32_t)t * qi28) & 0x0FFFFFFFu;
+      t = (uint64_t)m[k] * q28[0] + t;
+    } else {
+      zd[k - K] = (uint32_t)t & 0x0FFFFFFFu;
+    }
+    C = t >> 28;
+  });
+  zd[K - 1] = (uint32_t)C;
+  from28<L>(z, zd);
   // [0, 2q) -> [0, q)
   uint32_t u[D];
   lmask b;
@@ -155,6 +232,15 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
 #pragma unroll
   for (int i = 0; i < D; ++i) q[i] = a.q[i];
   const uint32_t qi = a.qinv32;
+#ifndef RG_WIDE_DIG28
+#define RG_WIDE_DIG28 1  // 0: the 32-bit-digit product (mont_wide), for A/B
+#endif
+  auto mont = [&](uint32_t(&z)[D], const uint32_t(&x)[D], const uint32_t(&y)[D]) {
+    if constexpr (RG_WIDE_DIG28)
+      mont28<L>(z, x, y, q, a.q28, a.qinv28);
+    else
+      mont_wide<D>(z, x, y, q, qi);
+  };
   // global element index of point x of tile sub-transform c (or -1 past the batch)
   auto elem = [&](int c, int x) -> long long {
     const long long s = s0 + c;
@@ -206,7 +292,7 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
       if constexpr (!INV) {  // ntt.go:254-259
         load_w();
         uint32_t t[D];
-        mont_wide<D>(t, v, w, q, qi);
+        mont(t, v, w);
         add_wide<D>(nu, u, t, q);
         sub_wide<D>(nv, u, t, q);
       } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
@@ -218,7 +304,7 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
         __builtin_amdgcn_sched_barrier(0);
         load_w();
-        mont_wide<D>(nv, d, w, q, qi);  // w = twInv / 2
+        mont(nv, d, w);  // w = twInv / 2
       }
 #pragma unroll
       for (int l = 0; l < L; ++l) {
