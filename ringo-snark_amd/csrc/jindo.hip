@@ -1768,49 +1768,62 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
 
 #pragma clang fp contract(on)
 
-// thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139)
+// thread = (commit, column, MLWE polynomial, coefficient pair) (prover.go:130-139).  Two
+// instantiations: ROUND = false covers the key columns (mlweSampler, one AES block and two table
+// searches per pair), ROUND = true the mask column (the rounded Gaussian with its exp / log), so
+// the table-search launch is not held at the rounded path's register count (238 VGPRs, 2 waves
+// per SIMD, when both were one kernel).
 constexpr int kMlweLdsTab = 512;  // mlweSampler's table in LDS up to this size (configs: 123 entries)
+template <bool ROUND>
 __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   __shared__ uint32_t lds[kAesLds];
   __shared__ uint32_t key[kKeyWords];
-  __shared__ uint64_t mtab[kMlweLdsTab];
+  __shared__ uint64_t mtab[ROUND ? 1 : kMlweLdsTab];
   aes_lds_fill(lds, a.te0);
-  aes_key_fill(key, a.key[kDomMlweRnd]);
   const bool tab_lds = a.cdt_mlwe.size <= kMlweLdsTab;  // else the binary search reads global memory
-  if (tab_lds)
+  if constexpr (ROUND) {
+    aes_key_fill(key, a.key[kDomMlweRnd]);
+  } else if (tab_lds) {
     for (int i = threadIdx.x; i < a.cdt_mlwe.size; i += blockDim.x) mtab[i] = a.cdt_mlwe.tables[i];
-  __syncthreads();
-  // grid-stride: a bounded grid fills the 64 KiB LDS tables once per workgroup, not once per 512 pairs
-  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.n_ml_pairs;
-       gid += (long long)gridDim.x * blockDim.x) {
-  const JShape& S = a.s;
-  const int nm = S.in_msis + S.mlwe;
-  const int m = (int)(gid % (S.d / 2));
-  const long long poly = gid / (S.d / 2);  // (b, col, j)
-  const int col = (int)((poly / nm) % (S.cols + 1));
-  long long* out = a.mlwe_noise + poly * S.d;
-  const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * nm + (unsigned long long)poly;
-  if (col != S.cols) {  // mlweSampler.Sample(0): centre 0, one table, no float tail
-    uint64_t w0, w1;
-    ks_words(a.key[kDomMlweCdt], gpoly, (uint64_t)m, lds, w0, w1);
-    int64_t v0, v1;
-    if (tab_lds) {
-      v0 = cdt_search(mtab, a.cdt_mlwe.size, w0);
-      v1 = cdt_search(mtab, a.cdt_mlwe.size, w1);
-    } else {
-      v0 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0);
-      v1 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1);
-    }
-    out[2 * m] = v0 + a.cdt_mlwe.tail_lo;
-    out[2 * m + 1] = v1 + a.cdt_mlwe.tail_lo;
-  } else {  // roundedSampler.Sample(0, maskMLWEStdDev)
-    for (int h = 0; h < 2; ++h) {
-      const int k = 2 * m + h;
-      Uniform u;
-      u.init(key, lds, gpoly * S.d + k);
-      out[k] = rounded_gauss(a.zig, u, 0.0, a.sd_mask_mlwe);
-    }
   }
+  __syncthreads();
+  const JShape& S = a.s;
+  const int nm = S.in_msis + S.mlwe, half = S.d / 2;
+  const int ncol = ROUND ? 1 : S.cols;  // columns this launch covers
+  const long long n = a.n_ml_pairs / (S.cols + 1) * ncol;
+  // grid-stride: a bounded grid fills the 64 KiB LDS tables once per workgroup, not once per 512 pairs
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < n;
+       gid += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(gid % half);
+    const long long r = gid / half;
+    const int j = (int)(r % nm);
+    const long long r2 = r / nm;
+    const int col = ROUND ? S.cols : (int)(r2 % S.cols);
+    const long long b = ROUND ? r2 : r2 / S.cols;
+    const long long poly = (b * (S.cols + 1) + col) * nm + j;  // (b, col, j)
+    long long* out = a.mlwe_noise + poly * S.d;
+    const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * nm + (unsigned long long)poly;
+    if constexpr (!ROUND) {  // mlweSampler.Sample(0): centre 0, one table, no float tail
+      uint64_t w0, w1;
+      ks_words(a.key[kDomMlweCdt], gpoly, (uint64_t)m, lds, w0, w1);
+      int64_t v0, v1;
+      if (tab_lds) {
+        v0 = cdt_search(mtab, a.cdt_mlwe.size, w0);
+        v1 = cdt_search(mtab, a.cdt_mlwe.size, w1);
+      } else {
+        v0 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w0);
+        v1 = cdt_search(a.cdt_mlwe.tables, a.cdt_mlwe.size, w1);
+      }
+      out[2 * m] = v0 + a.cdt_mlwe.tail_lo;
+      out[2 * m + 1] = v1 + a.cdt_mlwe.tail_lo;
+    } else {  // roundedSampler.Sample(0, maskMLWEStdDev)
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * m + h;
+        Uniform u;
+        u.init(key, lds, gpoly * S.d + k);
+        out[k] = rounded_gauss(a.zig, u, 0.0, a.sd_mask_mlwe);
+      }
+    }
   }
 }
 
@@ -2761,9 +2774,18 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
     RG_TRY(check_launch("jindo enc noise (COSAC)"));
   }
-  hipLaunchKernelGGL(mlwe_noise_kernel, dim3((unsigned)std::min<long long>((a.n_ml_pairs + 511) / 512, 1024)), dim3(512),
-                     0, st, a);
-  return check_launch("jindo mlwe noise");
+  {
+    const long long per_col = a.n_ml_pairs / (p.cols + 1);
+    if (p.cols > 0) {
+      const long long n = per_col * p.cols;
+      hipLaunchKernelGGL(mlwe_noise_kernel<false>, dim3((unsigned)std::min<long long>((n + 511) / 512, 1024)), dim3(512),
+                         0, st, a);
+      RG_TRY(check_launch("jindo mlwe noise (table)"));
+    }
+    hipLaunchKernelGGL(mlwe_noise_kernel<true>, dim3((unsigned)std::min<long long>((per_col + 511) / 512, 1024)),
+                       dim3(512), 0, st, a);
+  }
+  return check_launch("jindo mlwe noise (rounded)");
 }
 
 // scratch for the sampled randomness of `batch` commits
