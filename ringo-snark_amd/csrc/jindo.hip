@@ -1212,6 +1212,7 @@ struct SampleArgs {
   // cdf sum_{x = tailLo}^{j} rho(x - c/128) / norm for j = -1 .. size (host, Go's order)
   const double* cdt_sbound;
   const int* cdt_jmax;  // [128]: v0 <= jmax[c0] decides the sample as v0 (cdt2_noise_kernel)
+  int* wq;              // cdt2_noise_kernel's chunk counter (zeroed before the launch)
 };
 
 #pragma clang fp contract(off)
@@ -1345,7 +1346,22 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   const __attribute__((address_space(4))) double* dlt = (const __attribute__((address_space(4))) double*)a.delta;
   int i0 = 0;  // first nonzero deltaInv
   while (i0 < S.exp && dlt[i0] == 0.0) ++i0;
-  for (long long p0 = ((long long)blockIdx.x * kCdt2Waves + wl) * kCdtChunk; p0 < npoly; p0 += nw * kCdtChunk) {
+  (void)nw;
+#ifndef RG_CDT2_QUEUE
+#define RG_CDT2_QUEUE 1  // 0: the static chunk assignment (chunk w, w + waves, ...), for A/B
+#endif
+  // chunks from a counter: a wave that drew cheap polynomials (COSAC hand-offs, skipped ones)
+  // takes more, so the workgroups -- one per CU, whose last wave holds its CU -- end together
+  for (long long it = 0;; ++it) {
+    long long p0;
+    if constexpr (RG_CDT2_QUEUE) {
+      int ch = 0;
+      if (lane == 0) ch = atomicAdd(a.wq, 1);
+      p0 = (long long)__builtin_amdgcn_readlane(ch, 0) * kCdtChunk;
+    } else {
+      p0 = (((long long)blockIdx.x * kCdt2Waves + wl) + it * nw) * kCdtChunk;
+    }
+    if (p0 >= npoly) break;
     const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
     int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
     uint4 gnext = reinterpret_cast<const uint4*>(a.digits + p0 * 256)[lane];
@@ -2132,6 +2148,7 @@ __global__ __launch_bounds__(256) void dot2_kernel(FieldParams<L> F, const uint6
 struct rg_jindo_scratch {
   rg::DevBuf digits, com, ocom;
   rg::DevBuf last, mask, en, mn;  // the sampled randomness of rg_jindo_commit_sampled_dev
+  rg::DevBuf wq;                  // cdt2_noise_kernel's chunk counter
 };
 
 // Sampler setup (rg_jindo_set_stddevs): the reference's six standard deviations and the tables
@@ -2766,6 +2783,12 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     const unsigned g = (unsigned)std::min<long long>((npoly + kCdt2Waves - 1) / kCdt2Waves, 256);
     a.cdt_sbound = S.cdt_sbound.as<double>();
     a.cdt_jmax = S.cdt_jmax.as<int>();
+    if (!sc->wq.p) {
+      std::lock_guard<std::mutex> lk(J->mu);
+      RG_TRY(sc->wq.alloc(256));
+    }
+    a.wq = sc->wq.as<int>();
+    RG_HIP(hipMemsetAsync(a.wq, 0, sizeof(int), st));
     hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
     const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
