@@ -1212,7 +1212,7 @@ struct SampleArgs {
   // cdf sum_{x = tailLo}^{j} rho(x - c/128) / norm for j = -1 .. size (host, Go's order)
   const double* cdt_sbound;
   const int* cdt_jmax;  // [128]: v0 <= jmax[c0] decides the sample as v0 (cdt2_noise_kernel)
-  int* wq;              // cdt2_noise_kernel's chunk counter (zeroed before the launch)
+  int* wq;              // [0] cdt2_noise_kernel's chunk counter, [2..3] cosac2's job counter (zeroed)
 };
 
 #pragma clang fp contract(off)
@@ -1690,7 +1690,17 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
   const long long njobs = a.batch * per;
   const long long myjobs = njobs > wid ? (njobs - wid + nwaves - 1) / nwaves : 0;
   constexpr int NG = 256 / kCosGroup;  // groups per polynomial
-  const long long total = myjobs * NG;  // this wave's queue of groups
+#ifndef RG_COS2_CHUNKS
+#define RG_COS2_CHUNKS 1  // 0: each wave's fixed queue (jobs wid, wid + waves, ...), for A/B
+#endif
+  // RG_COS2_CHUNKS: a wave's queue is refilled kCos2Chunk jobs at a time from one counter (one
+  // atomic per chunk), so waves whose groups drew few words take more jobs; results do not depend
+  // on which wave draws a group
+  constexpr int kCos2Chunk = 4;
+  long long total = RG_COS2_CHUNKS ? 0 : myjobs * NG;  // this wave's queue of groups
+  long long job0 = 0;                                 // RG_COS2_CHUNKS: the chunk's first job
+  bool drained = false;                               // RG_COS2_CHUNKS: the counter passed njobs
+  unsigned long long* cq = reinterpret_cast<unsigned long long*>(a.wq + 2);
   const unsigned long long pbg = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * (unsigned long long)NG;
   auto mb = [](uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -1715,11 +1725,24 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
       // work computes the next block of the stream its state needs and steps on its first word
       for (;;) {
         const uint64_t need = __ballot(L.g < 0);
-        if (!need || next >= total) break;
+        if (!need) break;
+        if (next >= total) {
+          if (!RG_COS2_CHUNKS || drained) break;
+          unsigned long long base = 0;
+          if ((threadIdx.x & 63) == 0) base = atomicAdd(cq, (unsigned long long)kCos2Chunk);
+          job0 = (long long)(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), 0) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, 0));
+          if (job0 >= njobs) {
+            drained = true;
+            break;
+          }
+          next = 0;
+          total = (njobs - job0 < kCos2Chunk ? njobs - job0 : kCos2Chunk) * NG;
+        }
         const int rank = mb(need);
         if (L.g < 0 && next + rank < total) {
           const long long g = next + rank;
-          const long long job = wid + (g / NG) * nwaves;
+          const long long job = RG_COS2_CHUNKS ? job0 + g / NG : wid + (g / NG) * nwaves;
           const long long b = job / per;
           const int j = (int)(job % per);
           const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
@@ -2788,7 +2811,7 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
       RG_TRY(sc->wq.alloc(256));
     }
     a.wq = sc->wq.as<int>();
-    RG_HIP(hipMemsetAsync(a.wq, 0, sizeof(int), st));
+    RG_HIP(hipMemsetAsync(a.wq, 0, 4 * sizeof(int), st));  // [0]: cdt2's chunks, [2..3]: cosac2's jobs (u64)
     hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
     const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
