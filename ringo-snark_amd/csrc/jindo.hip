@@ -1259,7 +1259,7 @@ __device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
 #pragma clang fp contract(off)
 constexpr int kCdtLdsMaxSize = 96;  // tables' high words + guide in LDS when size <= 96 (<= 145 KiB
                                     // per workgroup with the 64 KiB AES table)
-constexpr int kCdtChunk = 32;       // consecutive polynomials per chunk
+constexpr int kCdtChunk = 8;        // consecutive polynomials per chunk (queue granularity; 32 / 16 / 8 A/B: profiles/r04q_queue_chunks_ab.txt)
 
 __device__ __forceinline__ double rl_f64(double x, int lane) {
   const uint64_t b = __double_as_longlong(x);
