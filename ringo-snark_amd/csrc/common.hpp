@@ -29,6 +29,7 @@ enum class Knob : int {
   JindoMac,    // RINGO_JINDO_MAC    h: mac3h, l: mac_kernel instead of the MFMA MAC
   JindoSplit,  // RINGO_JINDO_SPLIT  0: commit_sampled on the caller's stream only
   JindoEval,   // RINGO_JINDO_EVAL   mac: Evaluate's batch combination on mac_kernel, not dot_split_kernel
+  JindoUniTries,  // RINGO_JINDO_UNI_TRIES n: uniform_whole_kernel gives up after n tries (tests the fix-up path)
   Count
 };
 const char* knob(Knob k);

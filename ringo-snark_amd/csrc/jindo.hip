@@ -1953,6 +1953,93 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
   }();
 }
 
+// Whole-word draws (kbytes = 8 L, e.g. q255) within the first 8 KiB of each instance: a try is
+// L / 2 AES blocks in parallel, up to 1024 / L tries.  A draw that needs more (its probability is
+// 0.475^256 at q255) is left as all-ones -- never a value below q -- and flagged for
+// uniform_fix_kernel, so this kernel carries no XOR-accumulated refill: 112 VGPRs (4 waves/SIMD)
+// against the general kernel's 164 (2 waves/SIMD with its 64 KiB of LDS).
+template <int L>
+__global__ __launch_bounds__(512) void uniform_whole_kernel(UniArgs<L> a, int* flag, int max_tries) {
+  __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t key[kKeyWords];
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(key, a.key);
+  __syncthreads();
+  const JShape& S = a.s;
+  const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
+  const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
+       gid += (long long)gridDim.x * blockDim.x) {
+    const long long b = gid / per, i = gid % per;
+    uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
+    if (i == nl - 1) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) dst[l] = 0;
+      continue;
+    }
+    const unsigned long long inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
+    bool done = false;
+    for (int t = 0; t < max_tries; ++t) {
+      uint64_t z[L];
+#pragma unroll
+      for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, inst, (uint64_t)t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
+      z[L - 1] &= topm;  // the last byte's unused top bits (element.go:320-325)
+      if (!geq_q<L>(z, a.F)) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) dst[l] = z[l];
+        done = true;
+        break;
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) dst[l] = ~0ull;
+      *flag = 1;
+    }
+  }
+}
+
+// uniform_whole_kernel's leftovers: nothing unless a draw was flagged; then every all-ones element
+// is drawn again by the general kernel's loop, refill included
+template <int L>
+__global__ __launch_bounds__(512) void uniform_fix_kernel(UniArgs<L> a, const int* flag) {
+  if (*flag == 0) return;
+  __shared__ uint32_t lds[kAesLds];
+  __shared__ uint32_t key[kKeyWords];
+  aes_lds_fill(lds, a.te0);
+  aes_key_fill(key, a.key);
+  __syncthreads();
+  const JShape& S = a.s;
+  const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
+  const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
+       gid += (long long)gridDim.x * blockDim.x) {
+    const long long b = gid / per, i = gid % per;
+    uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
+    bool ones = i != nl - 1;
+#pragma unroll
+    for (int l = 0; l < L; ++l) ones = ones && dst[l] == ~0ull;
+    if (!ones) continue;
+    const unsigned long long inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
+    for (uint64_t t = 0;; ++t) {
+      uint64_t z[L];
+      if ((t + 1) * L <= 1024) {
+#pragma unroll
+        for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, inst, t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
+      } else {  // past the first 8 KiB buffer (uniform.go:64-82)
+#pragma unroll
+        for (int l = 0; l < L; ++l) z[l] = uniform_word_at(LdsKey{key}, lds, inst, t * L + l);
+      }
+      z[L - 1] &= topm;
+      if (!geq_q<L>(z, a.F)) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) dst[l] = z[l];
+        break;
+      }
+    }
+  }
+}
+
 // raw Sample() words of one UniformSampler instance (rg_uniform_words_dev)
 __global__ __launch_bounds__(512) void uniform_words_kernel(AesKey key, const uint32_t* te0, unsigned long long inst,
                                                             unsigned long long first, long long n, uint64_t* out) {
@@ -2718,7 +2805,7 @@ static rg_status make_keys(const rg_jindo_seeds* seeds, AesKey* keys) {
 
 template <int L>
 static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& key, unsigned long long first,
-                                uint64_t* last, uint64_t* mask, hipStream_t st) {
+                                uint64_t* last, uint64_t* mask, int* flag, hipStream_t st) {
   UniArgs<L> a;
   a.s = shape_of(J->p, 1);
   a.key = key;
@@ -2745,8 +2832,22 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.last_row = last;
   a.mask = mask;
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
-  hipLaunchKernelGGL(uniform_elems_kernel<L>, dim3((unsigned)std::min<long long>((a.total + 511) / 512, 1024)), dim3(512),
-                     0, st, a);
+  const dim3 ug((unsigned)std::min<long long>((a.total + 511) / 512, 1024));
+#ifndef RG_UNI_WHOLE
+#define RG_UNI_WHOLE 1  // 0: every draw on uniform_elems_kernel (A/B)
+#endif
+  if constexpr (L % 2 == 0 && RG_UNI_WHOLE) {
+    if (a.kbytes == 8 * L) {  // whole words: the common draws, then the (practically never) long ones
+      const char* kt = knob(Knob::JindoUniTries);  // experiments build: cap the tries (fix-up test)
+      const int tries = std::max(0, std::min(1024 / L, kt ? atoi(kt) : 1024 / L));
+      RG_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
+      hipLaunchKernelGGL(uniform_whole_kernel<L>, ug, dim3(512), 0, st, a, flag, tries);
+      RG_TRY(check_launch("jindo uniform (whole words)"));
+      hipLaunchKernelGGL(uniform_fix_kernel<L>, ug, dim3(512), 0, st, a, (const int*)flag);
+      return check_launch("jindo uniform (long draws)");
+    }
+  }
+  hipLaunchKernelGGL(uniform_elems_kernel<L>, ug, dim3(512), 0, st, a);
   return check_launch("jindo uniform");
 }
 
@@ -2772,12 +2873,17 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   memset(&a, 0, sizeof(a));
   RG_TRY(make_keys(seeds, a.key));
   rg_status s;
+  if (!sc->wq.p) {  // [0] cdt2's chunk counter, [2..3] cosac2's job counter, [4] uniform's long-draw flag
+    std::lock_guard<std::mutex> lk(J->mu);
+    RG_TRY(sc->wq.alloc(256));
+  }
+  int* uflag = sc->wq.as<int>() + 4;
   switch (p.field_limbs) {
-    case 1: s = launch_uniform<1>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
-    case 2: s = launch_uniform<2>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
-    case 4: s = launch_uniform<4>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
-    case 7: s = launch_uniform<7>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
-    default: s = launch_uniform<14>(J, batch, a.key[kDomUniform], first, d_last, d_mask, st); break;
+    case 1: s = launch_uniform<1>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
+    case 2: s = launch_uniform<2>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
+    case 4: s = launch_uniform<4>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
+    case 7: s = launch_uniform<7>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
+    default: s = launch_uniform<14>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
   }
   RG_TRY(s);
   RG_TRY(digits_stage(J, batch, d_v, nv, d_last, d_mask, digits, st));
@@ -2806,10 +2912,6 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     const unsigned g = (unsigned)std::min<long long>((npoly + kCdt2Waves - 1) / kCdt2Waves, 256);
     a.cdt_sbound = S.cdt_sbound.as<double>();
     a.cdt_jmax = S.cdt_jmax.as<int>();
-    if (!sc->wq.p) {
-      std::lock_guard<std::mutex> lk(J->mu);
-      RG_TRY(sc->wq.alloc(256));
-    }
     a.wq = sc->wq.as<int>();
     RG_HIP(hipMemsetAsync(a.wq, 0, 4 * sizeof(int), st));  // [0]: cdt2's chunks, [2..3]: cosac2's jobs (u64)
     hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);

@@ -41,6 +41,29 @@ def test_uniform_words_match_oracle(inst, first, n):
     assert (_h(out).view(np.uint64) == co.uniform_words(seed, inst, first, n)).all()
 
 
+@pytest.mark.parametrize("tries", [0, 1])
+def test_uniform_long_draws_fixup(tmp_path, tries):
+    """MustSetRandom's whole-word draws that uniform_whole_kernel leaves (all-ones, flagged) are
+    completed by uniform_fix_kernel with the same words: on the experiments build with
+    RINGO_JINDO_UNI_TRIES=0 (every draw goes to the fix-up) or 1 (the ~47% rejected on their first
+    try at q255 do), lastRow and mask still equal the oracle's draws (tests/exp_child.py)."""
+    import subprocess
+    import sys
+    name, B, first = "t10_b1", 2, 3
+    out = tmp_path / f"uni_{tries}.npz"
+    r = subprocess.run([sys.executable, os.path.join(HERE, "exp_child.py"), "uni", str(tries), str(out), name, str(B),
+                        str(first)], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(out)
+    P = PARAMS[name]
+    q = int(P["field_q_hex"], 16)
+    v = np.stack([make_v(q, P["rank"], seed=21 + b) for b in range(B)])
+    want = co.CJindo(P, q).sample([P[k] for k in SD_KEYS], pyref.delta_inv(P["base"], P["exp"]),
+                                  _seeds(b"uni-" + name.encode()).raw(), first, v)
+    assert (got["last_row"].view(np.uint64) == want["last_row"]).all()
+    assert (got["mask"].view(np.uint64) == want["mask"]).all()
+
+
 @pytest.mark.parametrize("name", ["t10_b1", "mult_t8193_b12"])
 def test_delta_inv_matches_bigfloat(name):
     P = PARAMS[name]

@@ -13,7 +13,7 @@ const char* knob(Knob k) {
   static const char* names[] = {"RINGO_NTT_KERNEL", "RINGO_NTT_CHUNK_MB", "RINGO_NTT_PREFETCH",
                                 "RINGO_NTT_WG_PER_CU", "RINGO_NTT_R8_PF", "RINGO_JINDO_PREP",
                                 "RINGO_JINDO_PREP_W", "RINGO_JINDO_MAC", "RINGO_JINDO_SPLIT",
-                                "RINGO_JINDO_EVAL"};
+                                "RINGO_JINDO_EVAL", "RINGO_JINDO_UNI_TRIES"};
   static_assert(sizeof(names) / sizeof(names[0]) == (size_t)Knob::Count, "knob names");
   const int i = (int)k;
   if (i < 0 || i >= (int)Knob::Count) return nullptr;
