@@ -195,14 +195,14 @@ def compute_floor(torch, ringo, q, L, N, batch, x, stream, steps, warmup):
     probe = 4 if L == 1 else 5
     ql = (ctypes.c_uint64 * L)(*[(q >> (64 * i)) & ((1 << 64) - 1) for i in range(L)])
     f, h = ctypes.c_void_p(), ctypes.c_void_p()
-    if E.rg_field_create(L, ql, ctypes.byref(f)) != 0 or E.rg_ntt_create(f, N, 1, ctypes.byref(h)) != 0:
-        return None
     p, s = ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(stream.cuda_stream)
 
     def pstep():
         assert E.rg_ntt_fwd_dev(h, p, p, batch, s) == 0 and E.rg_ntt_inv_dev(h, p, p, batch, s) == 0
 
-    try:
+    try:  # every handle created inside, destroyed in the finally whichever step failed
+        if E.rg_field_create(L, ql, ctypes.byref(f)) != 0 or E.rg_ntt_create(f, N, 1, ctypes.byref(h)) != 0:
+            return None
         if E.rg_set_probe(probe) != 0:
             return None
         for _ in range(max(2, warmup)):
@@ -217,8 +217,10 @@ def compute_floor(torch, ringo, q, L, N, batch, x, stream, steps, warmup):
         return evp.total_ms() / steps
     finally:
         E.rg_set_probe(0)
-        E.rg_ntt_destroy(h)
-        E.rg_field_destroy(f)
+        if h.value:
+            E.rg_ntt_destroy(h)
+        if f.value:
+            E.rg_field_destroy(f)
 
 
 def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world, eval_steps=0):

@@ -183,9 +183,10 @@ __device__ __forceinline__ uint32_t divstep_b2(uint32_t r, uint32_t n0, uint32_t
   return qt;
 }
 
-// x R^-1 mod q for a canonical x (Slice = fromMont, element.go): Montgomery reduction alone, L^2
-// word products instead of the 2 L^2 of f_mul(x, 1).  The result is canonical: (x + m q) / R < q + 1,
-// and equals q only when x = 0, which gives m = 0 and 0.
+// x R^-1 mod q (Slice = fromMont, element.go): Montgomery reduction alone, L^2 word products
+// instead of the 2 L^2 of f_mul(x, 1).  For any x < R, (x + m q) / R < q + 1, so one conditional
+// subtraction of q leaves the canonical residue (a non-canonical word such as x = q gives 0, as
+// f_mul(x, 1) did).
 template <int L>
 __device__ __forceinline__ void f_redc(uint64_t* z, const uint64_t* x, const FieldParams<L>& F) {
   uint64_t t[L];
@@ -212,8 +213,12 @@ __device__ __forceinline__ void f_redc(uint64_t* z, const uint64_t* x, const Fie
     }
     t[L - 1] = carry;
   }
+  uint64_t d[L];
+  uint32_t br = 0;
 #pragma unroll
-  for (int i = 0; i < L; ++i) z[i] = t[i];
+  for (int i = 0; i < L; ++i) d[i] = subb(t[i], F.q[i], br);
+#pragma unroll
+  for (int i = 0; i < L; ++i) z[i] = br ? t[i] : d[i];
 }
 
 template <int L>

@@ -23,6 +23,7 @@ struct rg_ntt {
   rg_field f;
   int N, logN, negacyclic;
   bool shoup, tiled;
+  bool halving = true;  // wide fields: rank_inv == N^-1 (finalize)
   std::vector<uint64_t> h_tw, h_twinv, h_ninv;  // Montgomery reps, [N][L]
   rg::DevBuf d_tw, d_twinv;                     // kernel format
   std::vector<rg::PassDesc> passes;             // forward order
@@ -211,6 +212,12 @@ static rg_status finalize(rg_ntt* t) {
     memcpy(t->nsc, &t->h_ninv[0], 8 * L);
     memcpy(t->w1n, w1n, 8 * L);
     t->nsc_sh = t->w1n_sh = 0;
+    // log N halvings give exactly N^-1: a table-built plan whose rank_inv is anything else keeps
+    // the per-stage inverse, which multiplies by the caller's rank_inv (ntt.go:242-243)
+    uint64_t n[16], ninv[16];
+    H.from_u64(n, (uint64_t)N);
+    H.inverse(ninv, n);
+    t->halving = H.eq(ninv, &t->h_ninv[0]);
   } else {
     RG_TRY(t->d_tw.upload(t->h_tw.data(), t->h_tw.size() * 8));
     RG_TRY(t->d_twinv.upload(t->h_twinv.data(), t->h_twinv.size() * 8));
@@ -237,6 +244,7 @@ static rg_status run(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t 
   p.shoup = t->shoup;
   p.inv = inv;
   p.tiled = t->tiled;
+  p.halving = t->halving;
   p.passes = t->passes.data();
   p.npasses = (int)t->passes.size();
   p.batch = batch;

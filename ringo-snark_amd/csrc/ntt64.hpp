@@ -360,6 +360,29 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
 //        L<->H pad (x>>5).
 // Every pattern pair was checked conflict-free for ds_*_b64 half-wave groups
 // (SQ_LDS_BANK_CONFLICT = 0 for COL in profiles/r01_ntt16_pmc_summary.txt).
+// Which exchanges cross waves (RG_NTT_WL = 1, the default): a wave holds lanes tid in [64w, 64w+64).
+//   ROW: s = tid >> 5, so a wave owns sub-transforms 2w, 2w + 1 whole, and every ROW address
+//        stays in its rows' [288 s, 288 s + 288): every ROW exchange is wave-private.
+//   COL: t >> 2 = w.  M and L put x bits [5, 8) = t >> 2 = w, i.e. the image block
+//        [576 w, 576 w + 576), so M <-> L is wave-private too; only H <-> M crosses waves.
+// A wave-private exchange needs no workgroup barrier: a wave's LDS operations execute in issue
+// order, so wave_lds_fence() (a compiler-level fence) orders its write-then-read and
+// read-then-overwrite.  The tile keeps workgroup barriers only for H <-> M in COL and for the
+// staged L-round twiddles `ltw`, which every wave reads (ROW, COL inverse: one barrier right
+// after the staging, whose global load is issued before the tile's data loads).
+#ifndef RG_NTT_WL
+#define RG_NTT_WL 0  // A/B knob, bit 0: ROW passes wave-local, bit 1: COL passes (0 = round-4 barriers)
+#endif
+#ifndef RG_NTT_STAGGER
+#define RG_NTT_STAGGER 0  // A/B knob: s_sleep argument per quarter of phase offset
+#endif
+#ifndef RG_NTT_YPRIO
+#define RG_NTT_YPRIO 0  // A/B knob: s_setprio for waves 4-7 of the workgroup
+#endif
+__device__ __forceinline__ void ntt_wave_fence() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0>
 __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw) {
   const uint32_t tid = threadIdx.x;
@@ -377,11 +400,31 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
+  constexpr bool WL = (RG_NTT_WL & (COL ? 2 : 1)) != 0;
   constexpr bool LTW = (COL || RP) && RG_NTT_LTW && (PROBE & 1) == 0;
-  if constexpr (LTW) {  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads)
-    const uint32_t base = COL ? 64u : 65536u + hi * 192u;
-    if (tid < 384u)
-      reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
+  // an exchange inside one wave's LDS block / one that crosses waves
+  auto wsync = [&]() {
+    if constexpr (WL) ntt_wave_fence();
+    else __syncthreads();
+  };
+  if constexpr (RG_NTT_STAGGER != 0) {  // first-generation workgroups of a CU start out of phase
+    if (tile < 1024u) {
+      const uint32_t k = (tile >> 8) & 3u;
+      for (uint32_t i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(RG_NTT_STAGGER);
+    }
+  }
+  if constexpr (RG_NTT_YPRIO != 0) {  // static priority for the workgroup's younger half (waves 4-7)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256u) __builtin_amdgcn_s_setprio(RG_NTT_YPRIO);
+  }
+  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads); WL: loaded before the
+  // tile's data (its wait then covers this load only) and written to LDS after they are issued
+  uint64_t ltw_word = 0;
+  const uint32_t ltw_base = COL ? 64u : 65536u + hi * 192u;
+  if constexpr (LTW && !WL) {
+    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
+  }
+  if constexpr (LTW && WL) {
+    if (tid < 384u) ltw_word = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
   }
   // ---- global load (RG_NTT_PRIO: the wave issues its tile loads at raised priority)
   if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(3);
@@ -405,6 +448,11 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   }
   if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(0);
   if constexpr (RG_NTT_PRIO == 2) __builtin_amdgcn_s_setprio(2);  // 2: butterflies at raised priority
+  if constexpr (LTW && WL) {
+    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = ltw_word;
+    // COL forward reads ltw only after its H -> M barrier
+    if constexpr (!COL || INV) __syncthreads();
+  }
   // PROBE & 4: the result stays live through a store that never fires (values are < 2q < 2^64 - 1)
   auto st64 = [&](uint64_t x, uint32_t voff, uint32_t soff) {
     if constexpr ((PROBE & 4) != 0) {
@@ -419,18 +467,19 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
                  rL8 = 288 * s + 8 * t + (t >> 2);
   if constexpr (!INV) {
     ntt16_round<3, 5, 0, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
-    // exchange H -> M
+    // exchange H -> M (COL: across waves)
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bH + 576 * y : rH + 36 * y] = e[y];
-    __syncthreads();
+    if constexpr (COL) __syncthreads();
+    else wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y];
     ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
-    __syncthreads();
+    wsync();
     // exchange M -> L
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)] = e[y];
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[COL ? bL + 16 * r : rL9 + r];
     ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
@@ -443,10 +492,10 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
       for (int r = 0; r < 8; ++r) st64(e[r], vo, (uint32_t)r << 11);
     } else {  // L -> H through LDS (pad x >> 5), then coalesced rows
-      __syncthreads();
+      wsync();
 #pragma unroll
       for (int r = 0; r < 8; ++r) lds[rL8 + r] = e[r];
-      __syncthreads();
+      wsync();
       const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
       for (int y = 0; y < 8; ++y) st64(lds[rH + 33 * y], vo + 256u * y, 0);
@@ -455,25 +504,26 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
 #pragma unroll
       for (int y = 0; y < 8; ++y) lds[rH + 33 * y] = e[y];
-      __syncthreads();
+      wsync();
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = lds[rL8 + r];
-      __syncthreads();
+      wsync();
     }
-    if constexpr (COL && LTW) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
+    if constexpr (COL && LTW && !WL) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
     ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     // exchange L -> M
 #pragma unroll
     for (int r = 0; r < 8; ++r) lds[COL ? bL + 16 * r : rL9 + r] = e[r];
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)];
     ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
-    __syncthreads();
-    // exchange M -> H
+    wsync();
+    // exchange M -> H (COL: across waves)
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y] = e[y];
-    __syncthreads();
+    if constexpr (COL) __syncthreads();
+    else wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bH + 576 * y : rH + 36 * y];
     ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);

@@ -11,7 +11,7 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
   const int logN = p.logN;
   const bool spare = (p.q[L - 1] >> 63) == 0;
   const char* k = knob(Knob::NttKernel);  // experiments build: RINGO_NTT_KERNEL=stage (A/B)
-  if (logN < 1 || logN > 16 || !spare || (k && k[0] == 's')) return run_stages<L, false>(p, st);
+  if (logN < 1 || logN > 16 || !spare || (p.inv && !p.halving) || (k && k[0] == 's')) return run_stages<L, false>(p, st);
   WideArgs a;
   memset(&a, 0, sizeof(a));
   // inverse: the halved copy of twInv that ntt.hip's finalize() appends to the table
@@ -20,8 +20,7 @@ static rg_status wide_run(const NttLaunch& p, hipStream_t st) {
     a.q[2 * l] = (uint32_t)p.q[l];
     a.q[2 * l + 1] = (uint32_t)(p.q[l] >> 32);
   }
-  a.qinv32 = (uint32_t)p.qinv;  // -q^-1 mod 2^64, so its low word is -q^-1 mod 2^32
-  a.qinv28 = a.qinv32 & 0x0FFFFFFFu;
+  a.qinv28 = (uint32_t)p.qinv & 0x0FFFFFFFu;  // -q^-1 mod 2^64, so its low 28 bits are -q^-1 mod 2^28
   for (int k = 0; k < 64 * L / 28; ++k) {  // q in 28-bit digits
     const int bit = 28 * k, l = bit >> 6, sh = bit & 63;
     uint64_t v = p.q[l] >> sh;

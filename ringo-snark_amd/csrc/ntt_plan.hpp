@@ -21,6 +21,7 @@ struct NttLaunch {
   uint64_t w1n_sh;
   int logN;
   bool shoup, inv, tiled;
+  bool halving;  // rank_inv == N^-1: the wide pass's per-stage halving scales the inverse correctly
   const PassDesc* passes;  // forward order
   int npasses;
   size_t batch;

@@ -10,9 +10,10 @@
 //     a workgroup loads `cpt` sub-transforms (2^P points at stride S) into limb-planar LDS, runs
 //     the P radix-2 stages with one butterfly per thread per step and a barrier between stages,
 //     and writes the tile back -- HBM sees one read and one write per element per pass;
-//   * the product is Montgomery on 32-bit digits (D = 2L), product scanning with a 96-bit column
-//     accumulator: one v_mad_u64_u32 with carry-out plus one v_addc per partial product, the
-//     quotient digit m_k = t_k (-q^-1) mod 2^32 per column: 2 D^2 products, no compares;
+//   * the product is Montgomery on 28-bit digits (mont28), product scanning with one 64-bit column
+//     accumulator: one v_mad_u64_u32 per partial product and no carry handling (the round-4
+//     32-bit-digit form, a v_mad_u64_u32 plus a v_addc per product, is
+//     tools/experiments/wide_mont32.patch);
 //   * every value stays canonical in [0, q) (one conditional subtract per add / sub / product:
 //     ~3 D operations against ~4 D^2 for the product), so limbs equal the reference's.
 // Twiddles are the reference's Montgomery tables tw[m + i] / twInv[m + i], read from L2.  The
@@ -25,7 +26,9 @@
 #pragma once
 #include <stdint.h>
 
-#include "madc.hpp"
+#include <type_traits>
+#include <utility>
+
 #include "ntt64.hpp"
 
 namespace rg {
@@ -38,7 +41,6 @@ struct WideArgs {
   uint64_t* out;
   const uint64_t* tw;  // Montgomery [N][L]: tw (forward) or twInv / 2 (inverse)
   uint32_t q[2 * kWideMaxL];
-  uint32_t qinv32;             // -q^-1 mod 2^32
   uint32_t q28[64 * kWideMaxL / 28];  // q in 28-bit digits (mont28)
   uint32_t qinv28;                    // -q^-1 mod 2^28
   int logN, G0, P, logS, cpt;  // pass: global stages [G0, G0 + P), points at stride 2^logS
@@ -47,58 +49,20 @@ struct WideArgs {
 
 #if defined(__HIPCC__)
 
-// z = x y 2^(-32 D) mod q, canonical, for canonical x, y and q < 2^(32 D - 1)
-template <int D>
-__device__ __forceinline__ void mont_wide(uint32_t (&z)[D], const uint32_t (&x)[D], const uint32_t (&y)[D],
-                                          const uint32_t (&q)[D], uint32_t qi) {
-  uint32_t m[D];
-  uint64_t A = 0;
-  uint32_t H = 0;
-  static_for<2 * D - 1>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    // two independent carry chains per column (x y products into A/H, m q products into B/G),
-    // interleaved in program order and merged once per column: one chain of dependent
-    // v_mad_u64_u32 leaves the SIMD idle at the 2 waves/SIMD the wide registers allow
-    constexpr int xlo = k < D ? 0 : k - D + 1, xhi = k < D ? k : D - 1;          // x y: i in [xlo, xhi]
-    constexpr int mlo = k < D ? 0 : k - D + 1, mhi = k < D ? k - 1 : D - 1;      // m q: i in [mlo, mhi], j >= 1
-    constexpr int nx = xhi - xlo + 1, nm = mhi >= mlo ? mhi - mlo + 1 : 0;
-    uint64_t B = 0;
-    uint32_t G = 0;
-    madc_column<nx, nm>(
-        A, H, B, G, [&](auto r) { return x[xlo + decltype(r)::value]; },
-        [&](auto r) { return y[k - xlo - decltype(r)::value]; }, [&](auto r) { return m[mlo + decltype(r)::value]; },
-        [&](auto r) { return q[k - mlo - decltype(r)::value]; });
-    if constexpr (nm > 0) {  // A/H += B/G
-      lmask c, c2, c3;
-      const uint32_t lo = add_co(lo32(A), lo32(B), c);
-      const uint32_t hi = addc_co(hi32(A), hi32(B), c, c2);
-      A = pk(lo, hi);
-      H = addc_co(H, G, c2, c3);
-    }
-    if constexpr (k < D) {  // quotient digit: clears the column's low word
-      m[k] = lo32(A) * qi;
-      lmask c, c2;
-      A = mad_co(m[k], q[0], A, c);
-      H = addc_co(H, 0u, c, c2);
-    } else {
-      z[k - D] = lo32(A);
-    }
-    A = pk(hi32(A), H);
-    H = 0;
-  });
-  z[D - 1] = lo32(A);
-  // [0, 2q) -> [0, q)
-  uint32_t u[D];
-  lmask b;
-  u[0] = sub_co(z[0], q[0], b);
-#pragma unroll
-  for (int i = 1; i < D; ++i) u[i] = subb_co(z[i], q[i], b, b);
-#pragma unroll
-  for (int i = 0; i < D; ++i) z[i] = sel(b, z[i], u[i]);
+// Compile-time loops: the products are hundreds of partial products, past what the loop unroller
+// fully unrolls, and a rolled loop indexes the digit arrays dynamically (s_set_gpr_idx).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// The same product on 28-bit digits (K = 64 L / 28: 16 for L = 7, 32 for L = 14; R = 2^(28 K) =
-// 2^(64 L), so the result is the same Montgomery product).  A 28-bit digit product is < 2^56,
+// z = x y 2^(-64 L) mod q, canonical, for canonical x, y and q < 2^(64 L - 1): Montgomery on
+// 28-bit digits (K = 64 L / 28: 16 for L = 7, 32 for L = 14; R = 2^(28 K) = 2^(64 L), so the
+// reference's Montgomery tables serve unchanged).  A 28-bit digit product is < 2^56,
 // so a column of up to 2 K products plus the carry stays below 2^63 in one 64-bit accumulator:
 // no carry-out per partial product (the 32-bit-digit form pays a v_addc for each), and the
 // products are plain C that hipcc schedules and pads itself.  Digits are cut from and packed
@@ -231,15 +195,8 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
   uint32_t q[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) q[i] = a.q[i];
-  const uint32_t qi = a.qinv32;
-#ifndef RG_WIDE_DIG28
-#define RG_WIDE_DIG28 1  // 0: the 32-bit-digit product (mont_wide), for A/B
-#endif
   auto mont = [&](uint32_t(&z)[D], const uint32_t(&x)[D], const uint32_t(&y)[D]) {
-    if constexpr (RG_WIDE_DIG28)
-      mont28<L>(z, x, y, q, a.q28, a.qinv28);
-    else
-      mont_wide<D>(z, x, y, q, qi);
+    mont28<L>(z, x, y, q, a.q28, a.qinv28);
   };
   // global element index of point x of tile sub-transform c (or -1 past the batch)
   auto elem = [&](int c, int x) -> long long {

@@ -60,6 +60,25 @@ def test_commit_matches_oracle(name, nvs):
         assert (com.Value == want["com"]).all(), (name, nv, "Commitment")
 
 
+def test_commit_noncanonical_v_reduces():
+    """A word of v equal to q (non-canonical; Montgomery q == 0) commits as 0 does: fromMont in
+    the digit encoder (encoder.go:149-158 via element.go's Slice) reduces fully, as gnark's
+    fromMont does for any word below R."""
+    P, q, params = _setup("t10_b1")
+    prv = jindo.NewProver(params, b"Jindo!")
+    L = (q.bit_length() + 63) // 64
+    v = make_v(q, 300, seed=3)
+    v[5] = 0
+    v[17] = [(q >> (64 * j)) & ((1 << 64) - 1) for j in range(L)]
+    vz = v.copy()
+    vz[17] = 0
+    rnd = make_randomness(P, q, seed=11)
+    com, op = prv.Commit(v, jindo.Randomness(**rnd))
+    comz, opz = prv.Commit(vz, jindo.Randomness(**rnd))
+    assert (op.Encode == opz.Encode).all()
+    assert (com.Value == comz.Value).all()
+
+
 @pytest.mark.parametrize("name", ["t10_b1", "t14_b1"])
 def test_commit_extreme_noise_matches_oracle(name):
     """Injected noise far outside the samplers' range (|s| up to 2^63 - 1, INT64_MIN + 1), which

@@ -208,3 +208,57 @@ def test_ntt_2e16_q255_bench_batch_spot_check(fields):
     T.inv_dev(x, x, B)
     torch.cuda.synchronize()
     assert torch.equal(x, ref)
+
+
+@pytest.mark.parametrize("name,B", [("zp440", 32), ("zp880", 16)])
+def test_ntt_2e16_wide_bench_batch_spot_check(fields, name, B):
+    """The wide Buckler fields at the batch bench.py's wide_ntt_* lines time (zp440 x 32,
+    zp880 x 16 polynomials of 2^16, in place; buckler_test.go:163-222 runs these fields): three
+    polynomials of the forward transform against the C oracle, so a forward that is consistently
+    wrong cannot hide behind the bench's fwd-then-inv self-check, then the in-place inverse
+    restores all B bit-exactly."""
+    import torch
+    q = fields[name]
+    N = 1 << 16
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, _, _ = cf.tables(N)
+    rng = np.random.default_rng(440 + B)
+    a = F.random(B * N, rng).reshape(B, N, F.L)
+    a[B - 1, N - 1] = F.mont([q - 1])[0]  # the largest residue
+    x = torch.from_numpy(a.view(np.int64).reshape(-1).copy()).cuda()
+    ref = x.clone()
+    T.fwd_dev(x, x, B)
+    torch.cuda.synchronize()
+    picks = [0, B // 2 + 1, B - 1]
+    want = cf.ntt_fwd(np.ascontiguousarray(a[picks]), tw)
+    got = x.cpu().numpy().view(np.uint64).reshape(B, N, F.L)
+    for j, i in enumerate(picks):
+        assert (got[i] == want[j]).all(), (name, i)
+    T.inv_dev(x, x, B)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+
+
+@pytest.mark.parametrize("name,logn", [("p63", 16), ("zp440", 10), ("zp880", 9), ("jindo_zp", 8)])
+def test_from_tables_honours_rank_inv(fields, name, logn):
+    """rg_ntt_create_from_tables takes Go's tables verbatim, rankInv included (ntt.go:86-87,
+    194-195 set it to N^-1; InvNTTTo multiplies by whatever the transformer holds,
+    ntt.go:242-243).  A plan built with another canonical rank_inv must scale by it, on every
+    kernel family: the wide fields' per-stage-halving pass only computes N^-1, so such a plan
+    takes the per-stage inverse instead."""
+    q = fields[name]
+    N = 1 << logn
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T0 = ringo.CyclotomicTransformer(F, N)
+    tw, twi, ninv = T0.tables()
+    rinv = F.mont([pow(3 * N, -1, q)])[0]  # (3N)^-1: a third of the reference's scaling
+    T = ringo.CyclotomicTransformer(F, N, tables=(tw, twi, rinv))
+    rng = np.random.default_rng(logn)
+    a = F.random(2 * N, rng).reshape(2, N, F.L)
+    got = T.InvNTTTo(None, a)
+    assert (got == cf.ntt_inv(a, twi, rinv)).all(), name
+    assert not (got == T0.InvNTTTo(None, a)).all()
+    assert (T.FwdNTTTo(None, a) == T0.FwdNTTTo(None, a)).all()
