@@ -1590,7 +1590,7 @@ int of_jindo_sample(const of_jindo* J, const double* sd, const double* delta, co
           uni_init(&U, &dom[0], gpoly);
           for (int k = 0; k < d; ++k) en[k] = cdt_sample(&ce, &U, -fp[k]);
         } else { /* cosac: an instance pair per group of G consecutive samples, drawn in order */
-          const int G = d < 16 ? d : 16;
+          const int G = d < 8 ? d : 8;  /* the library's partition (jindo.hip kCosGroup) */
           for (int g = 0; g < d / G; ++g) {
             of_uni B, R;
             uni_init(&B, &dom[1], gpoly * (uint64_t)(d / G) + (uint64_t)g);

@@ -360,16 +360,15 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const bool is_enc = job < a.n_enc;
   uint64_t* dst;
   if (is_enc) {
-    const long long b = job / ((long long)(S.cols + 1) * S.rows);
-    const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
-    dst = a.enc + job * nq * d;
+    const long long pj = job;
+    const int cr = (int)(pj % ((long long)(S.cols + 1) * S.rows));
+    dst = a.enc + pj * nq * d;
     if (enc_skipped(S, cr / S.rows, cr % S.rows)) {  // Opening.Encode[i][j] stays zero
       for (int k = tid; k < nq * d; k += blockDim.x) dst[k] = 0;
       return;
     }
-    const uint32_t* dg = a.digits + job * d;
-    const long long* nz = a.enc_noise + job * d;
-    (void)b;
+    const uint32_t* dg = a.digits + pj * d;
+    const long long* nz = a.enc_noise + pj * d;
     for (int k = tid; k < d; k += blockDim.x) {
       const long long c = nz[k];
       // the X^slots shift: coefficient k receives s[k - slots] (k >= slots) or -s[k + d - slots]
@@ -487,14 +486,15 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
   const uint32_t* dg = nullptr;
   const long long* nz;
   if (is_enc) {
-    const int cr = (int)(job % ((long long)(S.cols + 1) * S.rows));
-    dst = a.enc + job * nq * 256;
+    const long long pj = job;
+    const int cr = (int)(pj % ((long long)(S.cols + 1) * S.rows));
+    dst = a.enc + pj * nq * 256;
     if (enc_skipped(S, cr / S.rows, cr % S.rows)) {  // Opening.Encode[i][j] stays zero
       for (int k = (int)lane; k < nq * 256; k += 64) dst[k] = 0;
       return;
     }
-    dg = a.digits + job * 256;
-    nz = a.enc_noise + job * 256;
+    dg = a.digits + pj * 256;
+    nz = a.enc_noise + pj * 256;
   } else {
     const long long mj = job - a.n_enc;
     dst = a.mlwe + mj * nq * 256;
@@ -1196,7 +1196,10 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
 // prover's sequence, so batches and ranks never share keystream.
 // ------------------------------------------------------------------------------------------
 enum { kDomEncCdt = 0, kDomCosac, kDomCosacRnd, kDomMlweCdt, kDomMlweRnd, kDomUniform, kNumDom };
-constexpr int kCosGroup = 16;  // COSAC samples per sampler-instance pair (d >= 16; d < 16: d)
+// COSAC samples per sampler-instance pair.  8, not 16 (round 4): a wave's 64 lanes then fill from
+// 2 polynomials, so cosac2's queue hands out work in half the size and its end-of-launch tail halves
+// (configs[2] 61.3 K -> 62.4 K commits/s with the stream DAG, profiles/r05h_dag_ab.txt)
+constexpr int kCosGroup = 8;
 
 struct SampleArgs {
   JShape s;
@@ -1317,6 +1320,71 @@ __host__ __device__ constexpr int cdt_key_off(int size) { return cdt_guide_off(s
 //    order; 2^-40 covers both libms and the float sums).  Outside that band the comparison is
 //    decided; inside it (p within 1e-12 of the sum: p ~ 1, unseen in practice) the wave sums the
 //    terms in the reference's order.  Results equal the reference's draw for draw.
+// deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order) from the
+// polynomial's 256 digits in the wave's LDS slot dl: coefficient k reads digit (k + (i+1) slots)
+// mod 256, added when that index wrapped; fp = the negated centres.  Leading zero deltas (12 of 16
+// at the configs' shapes: b^i / p underflows the double grid) are skipped (i0); later zeros are
+// added: fp starts at +0 and never becomes -0, so adding 0 * g changes nothing, and four digits'
+// loads are in flight at once.  One definition for both kernels that need centres, so TwinCDT
+// and COSAC polynomials see the same arithmetic (fp contract off).
+typedef const __attribute__((address_space(4))) double* dconst_ptr;
+__device__ __forceinline__ void enc_centres(const uint4* dl, int lane, const JShape& S, dconst_ptr dlt, int i0,
+                                            double (&fp)[4]) {
+  fp[0] = fp[1] = fp[2] = fp[3] = 0.0;
+  auto cstep = [&](double di, int i, const uint4& q) {
+    // slots % 4 == 0 (the launch condition) makes base a multiple of 4: base + h >= 256 for
+    // all four coefficients or for none, so one sign per digit; fp + (-di) g == fp - di g
+    const double sdi = 4 * lane + (i + 1) * S.slots >= 256 ? di : -di;
+    fp[0] = fp[0] + sdi * (double)q.x;
+    fp[1] = fp[1] + sdi * (double)q.y;
+    fp[2] = fp[2] + sdi * (double)q.z;
+    fp[3] = fp[3] + sdi * (double)q.w;
+  };
+  auto dslot = [&](int i) { return dl[((4 * lane + (i + 1) * S.slots) & 255) >> 2]; };
+  int i = i0;
+  for (; i + 4 <= S.exp; i += 4) {
+    const uint4 q0 = dslot(i), q1 = dslot(i + 1), q2 = dslot(i + 2), q3 = dslot(i + 3);
+    const double d0 = dlt[i], d1 = dlt[i + 1], d2 = dlt[i + 2], d3 = dlt[i + 3];
+    cstep(d0, i, q0);
+    cstep(d1, i + 1, q1);
+    cstep(d2, i + 2, q2);
+    cstep(d3, i + 3, q3);
+  }
+  for (; i < S.exp; ++i) cstep(dlt[i], i, dslot(i));
+}
+
+// The COSAC polynomials' centres (row 0 of the data columns, every row of the mask column: the
+// stddevs other than ecdStdDev, prover.go:93-123), written as doubles into enc_noise for
+// cosac2_noise_kernel: one wave per polynomial, jobs in cosac2's order.  A launch of its own
+// (not part of cdt2_noise_kernel) so that the TwinCDT and COSAC samplers are independent and
+// can run on two streams, each filling the other's tail.
+constexpr int kCentreWaves = 4;
+__global__ __launch_bounds__(64 * kCentreWaves) void cos_centre_kernel(SampleArgs a) {
+  __shared__ uint4 dls[kCentreWaves][64];
+  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const JShape& S = a.s;
+  const int per = S.cols + S.rows;
+  const long long job = (long long)blockIdx.x * kCentreWaves + wl;
+  if (job >= a.batch * per) return;
+  const long long b = job / per;
+  const int j = (int)(job % per);
+  const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
+  const double sd = col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
+  if (enc_skipped(S, col, row) || sd == a.sd_ecd) return;  // cdt2_noise_kernel's polynomials
+  const long long poly = (b * (S.cols + 1) + col) * S.rows + row;
+  const dconst_ptr dlt = (dconst_ptr)a.delta;
+  int i0 = 0;
+  while (i0 < S.exp && dlt[i0] == 0.0) ++i0;
+  uint4* dl = dls[wl];
+  dl[lane] = reinterpret_cast<const uint4*>(a.digits + poly * 256)[lane];
+  wave_lds_fence();
+  double fp[4];
+  enc_centres(dl, lane, S, dlt, i0, fp);
+  double2* out = reinterpret_cast<double2*>(a.enc_noise + poly * 256);
+  out[2 * lane] = make_double2(-fp[0], -fp[1]);
+  out[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
+}
+
 constexpr int kCdt2Waves = 16;
 __host__ __device__ constexpr int cdt2_dig_off(int size) { return cdt_key_off(size) + kKeyWords * 4; }
 __host__ __device__ constexpr int cdt2_jmax_off(int size) { return cdt2_dig_off(size) + kCdt2Waves * 1024; }
@@ -1342,16 +1410,16 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   const JShape& S = a.s;
   const long long npoly = a.batch * (S.cols + 1) * S.rows;
   const long long nw = (long long)gridDim.x * kCdt2Waves;
+  (void)nw;
   const double norm = sqrt(2.0 * M_PI) * C.sigma;
   const double two_s2 = 2.0 * C.sigma * C.sigma;
   const LdsKey key{keyl};
   const int sstride = n + 2;
   // deltaInv through the constant address space: scalar loads (a plain global load waits on
   // vmcnt(0) per digit, as the kernel's stores defeat the no-clobber analysis)
-  const __attribute__((address_space(4))) double* dlt = (const __attribute__((address_space(4))) double*)a.delta;
+  const dconst_ptr dlt = (dconst_ptr)a.delta;
   int i0 = 0;  // first nonzero deltaInv
   while (i0 < S.exp && dlt[i0] == 0.0) ++i0;
-  (void)nw;
 #ifndef RG_CDT2_QUEUE
 #define RG_CDT2_QUEUE 1  // 0: the static chunk assignment (chunk w, w + waves, ...), for A/B
 #endif
@@ -1385,41 +1453,12 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       }
       const double sd =
           col == S.cols ? (row == 0 ? a.sd_mask_blind : a.sd_mask) : (row == 0 ? a.sd_ecd_blind : a.sd_ecd);
-      const bool cdt = sd == a.sd_ecd;
+      if (sd != a.sd_ecd) continue;  // a COSAC polynomial: cos_centre_kernel writes its centres
       dl[lane] = g;
       wave_lds_fence();
-      // deltaInv centres of coefficients 4 lane + h (encoder.go:153-165, Go's summation order):
-      // coefficient k reads digit (k + (i+1) slots) mod 256, added when that index wrapped
-      double fp[4] = {0.0, 0.0, 0.0, 0.0};
-      // Leading zero deltas (12 of 16 at the configs' shapes: b^i / p underflows the double
-      // grid) are skipped once per kernel (i0); later zeros are added: fp starts at +0 and never
-      // becomes -0, so adding 0 * g changes nothing, and four digits' loads are in flight at once.
-      auto cstep = [&](double di, int i, const uint4& q) {
-        // slots % 4 == 0 (the launch condition) makes base a multiple of 4: base + h >= 256 for
-        // all four coefficients or for none, so one sign per digit; fp + (-di) g == fp - di g
-        const double sdi = 4 * lane + (i + 1) * S.slots >= 256 ? di : -di;
-        fp[0] = fp[0] + sdi * (double)q.x;
-        fp[1] = fp[1] + sdi * (double)q.y;
-        fp[2] = fp[2] + sdi * (double)q.z;
-        fp[3] = fp[3] + sdi * (double)q.w;
-      };
-      auto dslot = [&](int i) { return dl[((4 * lane + (i + 1) * S.slots) & 255) >> 2]; };
-      int i = i0;
-      for (; i + 4 <= S.exp; i += 4) {
-        const uint4 q0 = dslot(i), q1 = dslot(i + 1), q2 = dslot(i + 2), q3 = dslot(i + 3);
-        const double d0 = dlt[i], d1 = dlt[i + 1], d2 = dlt[i + 2], d3 = dlt[i + 3];
-        cstep(d0, i, q0);
-        cstep(d1, i + 1, q1);
-        cstep(d2, i + 2, q2);
-        cstep(d3, i + 3, q3);
-      }
-      for (; i < S.exp; ++i) cstep(dlt[i], i, dslot(i));
+      double fp[4];
+      enc_centres(dl, lane, S, dlt, i0, fp);
       wave_lds_fence();  // the slot is rewritten for the next polynomial after these reads
-      if (!cdt) {  // a COSAC polynomial: hand the centres to cosac2_noise_kernel
-        reinterpret_cast<double2*>(out)[2 * lane] = make_double2(-fp[0], -fp[1]);
-        reinterpret_cast<double2*>(out)[2 * lane + 1] = make_double2(-fp[2], -fp[3]);
-        continue;
-      }
       const unsigned long long gpoly =
           a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
       uint64_t u[4];
@@ -1701,7 +1740,7 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
   // RG_COS2_CHUNKS: a wave's queue is refilled kCos2Chunk jobs at a time from one counter (one
   // atomic per chunk), so waves whose groups drew few words take more jobs; results do not depend
   // on which wave draws a group
-  constexpr int kCos2Chunk = 4;
+  constexpr int kCos2Chunk = 64 / NG;  // jobs per refill: one group per lane of the wave
   long long total = RG_COS2_CHUNKS ? 0 : myjobs * NG;  // this wave's queue of groups
   long long job0 = 0;                                 // RG_COS2_CHUNKS: the chunk's first job
   bool drained = false;                               // RG_COS2_CHUNKS: the counter passed njobs
@@ -2294,11 +2333,20 @@ struct rg_jindo {
   std::mutex mu;  // guards `scratch` and `aux`
   std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
   rg_jindo_samplers smp;
-  // second stream of the sampled commit's two-way split, one per caller stream (lazily created), so
-  // that its scratch (keyed by the aux stream) belongs to that caller stream alone
-  std::map<hipStream_t, hipStream_t> aux;
+  // the sampled commit's helper streams and events, one set per caller stream (lazily created):
+  // s[0] runs the COSAC centres + cosac2, s[1] the MLWE samplers and their prep (commit_sampled_dev)
+  struct Aux {
+    hipStream_t s[2] = {nullptr, nullptr};
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+  };
+  std::map<hipStream_t, Aux> aux;
   ~rg_jindo() {
-    for (auto& kv : aux) (void)hipStreamDestroy(kv.second);
+    for (auto& kv : aux) {
+      for (hipStream_t x : kv.second.s)
+        if (x) (void)hipStreamDestroy(x);
+      for (hipEvent_t x : kv.second.e)
+        if (x) (void)hipEventDestroy(x);
+    }
   }
 };
 
@@ -2736,10 +2784,11 @@ static rg_status digits_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   }
 }
 
-// 2.-5. from the digits and the randomness: encode tails + MLWE finalize with their NTTs, then the core
-static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const uint32_t* digits, const int64_t* d_en,
-                                    const int64_t* d_mn, uint64_t* d_incom, uint64_t* d_enc, uint64_t* d_mlwe,
-                                    uint64_t* d_com, rg_jindo_scratch* sc, hipStream_t st) {
+// 2. encode tails + MLWE finalize with their NTTs (prep256_kernel): jobs [0, n_enc) are the encode
+// polynomials, [n_enc, n_enc + n_ml) the MLWE ones; `part` selects both or one of the two sets
+enum PrepPart { kPrepAll = 3, kPrepEnc = 1, kPrepMlwe = 2 };
+static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_t* digits, const int64_t* d_en,
+                             const int64_t* d_mn, uint64_t* d_enc, uint64_t* d_mlwe, int part, hipStream_t st) {
   const rg_jindo_params& p = J->p;
   const int d = p.d, nq = p.nq, nm = p.in_msis + p.mlwe;
   PrepArgs pa;
@@ -2750,10 +2799,11 @@ static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const 
   pa.mlwe_noise = reinterpret_cast<const long long*>(d_mn);
   pa.enc = d_enc;
   pa.mlwe = d_mlwe;
-  pa.n_enc = (long long)batch * (p.cols + 1) * p.rows;
-  const long long n_ml = (long long)batch * (p.cols + 1) * nm;
+  pa.n_enc = (part & kPrepEnc) ? (long long)batch * (p.cols + 1) * p.rows : 0;
+  const long long n_ml = (part & kPrepMlwe) ? (long long)batch * (p.cols + 1) * nm : 0;
   pa.n_ml = n_ml;
   pa.clim = (long long)(((uint64_t)1 << 61) / p.base);
+  if (pa.n_enc + n_ml == 0) return RG_OK;
   bool q61 = true;  // prep256's lazy [0, 8q) needs q < 2^61 (every configs ring prime is <= 59 bits)
   for (int l = 0; l < nq; ++l) q61 = q61 && J->rq[l].q < (1ull << 61);
   if (d == 256 && q61 && !prep_legacy()) {
@@ -2772,7 +2822,14 @@ static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const 
   } else {
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   }
-  RG_TRY(check_launch("jindo prep"));
+  return check_launch("jindo prep");
+}
+
+// 2.-5. from the digits and the randomness: encode tails + MLWE finalize with their NTTs, then the core
+static rg_status commit_from_digits(rg_jindo* J, size_t batch, size_t nv, const uint32_t* digits, const int64_t* d_en,
+                                    const int64_t* d_mn, uint64_t* d_incom, uint64_t* d_enc, uint64_t* d_mlwe,
+                                    uint64_t* d_com, rg_jindo_scratch* sc, hipStream_t st) {
+  RG_TRY(prep_launch(J, batch, nv, digits, d_en, d_mn, d_enc, d_mlwe, kPrepAll, st));
   return commit_core(J, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
 }
 
@@ -2857,9 +2914,17 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
 }
 
 // lastRow/mask (crypto/rand), then digits, then every Gaussian sample of the batch
+// Streams: st runs MustSetRandom, the digits and TwinCDT (cdt2); s_cos, once the digits are done
+// (event e_dig), the COSAC centres and cosac2; s_ml, once st reaches this call (event e_start),
+// the MLWE samplers, which need neither.  s_cos / s_ml may be st itself (one stream, no events).
+// The caller joins s_cos and s_ml back into st before it reads their outputs.
 static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const rg_jindo_seeds* seeds,
                               unsigned long long first, uint64_t* d_last, uint64_t* d_mask, int64_t* d_en,
-                              int64_t* d_mn, uint32_t* digits, rg_jindo_scratch* sc, hipStream_t st) {
+                              int64_t* d_mn, uint32_t* digits, rg_jindo_scratch* sc, hipStream_t st,
+                              hipStream_t s_cos = nullptr, hipStream_t s_ml = nullptr, hipEvent_t e_start = nullptr,
+                              hipEvent_t e_dig = nullptr) {
+  if (!s_cos) s_cos = st;
+  if (!s_ml) s_ml = st;
   const rg_jindo_params& p = J->p;
   if (!J->smp.ready) {
     set_last_error("rg_jindo_set_stddevs was not called on this handle");
@@ -2883,6 +2948,10 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     RG_TRY(sc->wq.alloc(256));
   }
   int* uflag = sc->wq.as<int>() + 4;
+  if (s_ml != st) {
+    RG_HIP(hipEventRecord(e_start, st));
+    RG_HIP(hipStreamWaitEvent(s_ml, e_start, 0));
+  }
   switch (p.field_limbs) {
     case 1: s = launch_uniform<1>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
     case 2: s = launch_uniform<2>(J, batch, a.key[kDomUniform], first, d_last, d_mask, uflag, st); break;
@@ -2919,24 +2988,31 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     a.cdt_jmax = S.cdt_jmax.as<int>();
     a.wq = sc->wq.as<int>();
     RG_HIP(hipMemsetAsync(a.wq, 0, 4 * sizeof(int), st));  // [0]: cdt2's chunks, [2..3]: cosac2's jobs (u64)
+    if (s_cos != st) {
+      RG_HIP(hipEventRecord(e_dig, st));
+      RG_HIP(hipStreamWaitEvent(s_cos, e_dig, 0));
+    }
     hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
     const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
+    hipLaunchKernelGGL(cos_centre_kernel, dim3((unsigned)((ncos + kCentreWaves - 1) / kCentreWaves)),
+                       dim3(64 * kCentreWaves), 0, s_cos, a);
+    RG_TRY(check_launch("jindo enc noise (COSAC centres)"));
     const long long w2 = kCos2Threads / 64;
     const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
-    hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, st, a);
+    hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, s_cos, a);
     RG_TRY(check_launch("jindo enc noise (COSAC)"));
   }
   {
     const long long per_col = a.n_ml_pairs / (p.cols + 1);
     if (p.cols > 0) {
       const long long n = per_col * p.cols;
-      hipLaunchKernelGGL(mlwe_noise_kernel<false>, dim3((unsigned)std::min<long long>((n + 511) / 512, 1024)), dim3(512),
-                         0, st, a);
+      hipLaunchKernelGGL(mlwe_noise_kernel<false>, dim3((unsigned)std::min<long long>((n + 511) / 512, 1024)),
+                         dim3(512), 0, s_ml, a);
       RG_TRY(check_launch("jindo mlwe noise (table)"));
     }
     hipLaunchKernelGGL(mlwe_noise_kernel<true>, dim3((unsigned)std::min<long long>((per_col + 511) / 512, 1024)),
-                       dim3(512), 0, st, a);
+                       dim3(512), 0, s_ml, a);
   }
   return check_launch("jindo mlwe noise (rounded)");
 }
@@ -3783,50 +3859,45 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
   RG_TRY(on_device(J));
   rg_jindo* Jm = const_cast<rg_jindo*>(J);
   hipStream_t st = as_stream(stream);
-  auto run = [&](size_t b0, size_t nb, hipStream_t s) -> rg_status {  // commits [b0, b0 + nb) on s
-    const rg_jindo_params& p = J->p;
-    const size_t d = p.d, nm = p.in_msis + p.mlwe;
-    rg_jindo_scratch* sc = nullptr;
-    RG_TRY(stream_scratch(Jm, nb, s, &sc));
-    RG_TRY(sample_scratch(Jm, nb, sc, s));
-    uint32_t* digits = sc->digits.as<uint32_t>();
-    RG_TRY(sample_stage(Jm, nb, d_v + b0 * nv * p.field_limbs, nv, seeds, first_commit + b0, sc->last.as<uint64_t>(),
-                        sc->mask.as<uint64_t>(), sc->en.as<int64_t>(), sc->mn.as<int64_t>(), digits, sc, s));
-    return commit_from_digits(Jm, nb, nv, digits, sc->en.as<int64_t>(), sc->mn.as<int64_t>(),
-                              d_incom + b0 * p.dcmp * p.nqo * d, d_enc + b0 * (p.cols + 1) * p.rows * p.nq * d,
-                              d_mlwe + b0 * (p.cols + 1) * nm * p.nq * d, d_com + b0 * p.out_msis * p.nq * d, sc, s);
-  };
-  // Two halves on two streams (the caller's and the handle's auxiliary one, joined by events):
-  // the samplers (LDS / AES-latency bound) of one half overlap the other half's VALU-bound core
-  // (tools/stream_overlap.py: +4-5% commits/s).  Results are identical: sampler instances are
-  // numbered per commit (first_commit + b0), scratch is per stream, and the aux stream (with its
-  // scratch) belongs to this caller stream only, so concurrent callers on different streams never
-  // share a buffer.
-  static const bool no_split = [] {  // RINGO_JINDO_SPLIT=0: one stream (per-kernel profiling)
+  rg_jindo_scratch* sc = nullptr;
+  RG_TRY(stream_scratch(Jm, batch, st, &sc));
+  RG_TRY(sample_scratch(Jm, batch, sc, st));
+  uint32_t* digits = sc->digits.as<uint32_t>();
+  int64_t *en = sc->en.as<int64_t>(), *mn = sc->mn.as<int64_t>();
+  // The batch as one DAG over three streams (the caller's st and two helpers of this caller
+  // stream), so that each sampler's tail overlaps other work instead of idling the chip:
+  //   st:   MustSetRandom -> digits -> cdt2 (TwinCDT) ...................... -> prep(encode) -> core
+  //   s[0]:                    (digits) -> COSAC centres -> cosac2 ----------^
+  //   s[1]: mlwe samplers -> prep(MLWE) -------------------------------------^
+  // Results do not depend on the schedule: every sampler instance is numbered per commit, and
+  // each buffer has one writer ordered before its readers by the events.
+  static const bool one_stream = [] {  // RINGO_JINDO_SPLIT=0: everything on st (per-kernel profiling)
     const char* e = knob(Knob::JindoSplit);
     return e && e[0] == '0';
   }();
-  if (batch < 64 || no_split) return run(0, batch, st);
-  hipStream_t aux;
-  {
+  rg_jindo::Aux* ax = nullptr;
+  if (!one_stream) {
     std::lock_guard<std::mutex> lk(Jm->mu);
-    hipStream_t& a = Jm->aux[st];
-    if (!a) RG_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
-    aux = a;
+    rg_jindo::Aux& x = Jm->aux[st];
+    for (hipStream_t& s : x.s)
+      if (!s) RG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (hipEvent_t& e : x.e)
+      if (!e) RG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ax = &x;
   }
-  hipEvent_t e0, e1;
-  RG_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
-  RG_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-  RG_HIP(hipEventRecord(e0, st));
-  RG_HIP(hipStreamWaitEvent(aux, e0, 0));  // the inputs are ready on the caller's stream
-  const size_t h0 = batch / 2;
-  rg_status s0 = run(0, h0, st);
-  rg_status s1 = s0 == RG_OK ? run(h0, batch - h0, aux) : s0;
-  RG_HIP(hipEventRecord(e1, aux));
-  RG_HIP(hipStreamWaitEvent(st, e1, 0));  // the caller's stream sees every output
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return s1;
+  hipStream_t s_cos = ax ? ax->s[0] : st, s_ml = ax ? ax->s[1] : st;
+  RG_TRY(sample_stage(Jm, batch, d_v, nv, seeds, first_commit, sc->last.as<uint64_t>(), sc->mask.as<uint64_t>(), en, mn,
+                      digits, sc, st, s_cos, s_ml, ax ? ax->e[0] : nullptr, ax ? ax->e[1] : nullptr));
+  RG_TRY(prep_launch(Jm, batch, nv, digits, en, mn, d_enc, d_mlwe, kPrepMlwe, s_ml));
+  // (the TwinCDT rows' prep right behind cdt2, beside cosac2, measured no faster: r05i)
+  if (ax) {  // join: the encode prep needs both samplers' noise; the core needs the MLWE prep
+    RG_HIP(hipEventRecord(ax->e[2], s_cos));
+    RG_HIP(hipEventRecord(ax->e[3], s_ml));
+    RG_HIP(hipStreamWaitEvent(st, ax->e[2], 0));
+    RG_HIP(hipStreamWaitEvent(st, ax->e[3], 0));
+  }
+  RG_TRY(prep_launch(Jm, batch, nv, digits, en, mn, d_enc, d_mlwe, kPrepEnc, st));
+  return commit_core(Jm, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
 }
 
 rg_status rg_jindo_release_stream(rg_jindo* J, void* stream) {
@@ -3837,9 +3908,14 @@ rg_status rg_jindo_release_stream(rg_jindo* J, void* stream) {
   RG_HIP(hipStreamSynchronize(st));
   auto a = J->aux.find(st);
   if (a != J->aux.end()) {
-    RG_HIP(hipStreamSynchronize(a->second));
-    J->scratch.erase(a->second);
-    (void)hipStreamDestroy(a->second);
+    for (hipStream_t x : a->second.s)
+      if (x) {
+        RG_HIP(hipStreamSynchronize(x));
+        J->scratch.erase(x);
+        (void)hipStreamDestroy(x);
+      }
+    for (hipEvent_t x : a->second.e)
+      if (x) (void)hipEventDestroy(x);
     J->aux.erase(a);
   }
   J->scratch.erase(st);
