@@ -296,8 +296,8 @@ rg_status rg_jindo_delta_inv(const rg_jindo* j, double* out);
  * MustSetRandom (prover.go:65-139, encoder.go:149-183).  A Go caller draws them from crypto/rand.
  * On the device each sampler instance is a window of its domain's counter space (instance n =
  * the UniformSampler with IV + n 2^24, a 128-bit sum, so the 2^64 instance numbers have disjoint
- * windows): one per encode polynomial (twinCDT), per group of 16 consecutive coefficients of a
- * COSAC-encoded polynomial (COSAC and its RoundedGaussianSampler, instance poly (d/16) + group),
+ * windows): one per encode polynomial (twinCDT), per group of 8 consecutive coefficients of a
+ * COSAC-encoded polynomial (COSAC and its RoundedGaussianSampler, instance poly (d/8) + group),
  * per MLWE polynomial (mlweSampler), per mask-column MLWE sample (rounded) and per field element
  * (uniform), numbered from `first_commit`, the index of
  * the batch's first commit among all commits made with these seeds (so batches and GPUs never
@@ -317,10 +317,10 @@ rg_status rg_jindo_sample_dev(const rg_jindo* j, size_t batch, const uint64_t* d
                               const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_last_row,
                               uint64_t* d_mask, int64_t* d_enc_noise, int64_t* d_mlwe_noise, void* stream);
 /* Prover.Commit end to end on the device (prover.go:45-202): rg_jindo_sample_dev, then
- * rg_jindo_commit_dev on that randomness (kept in the stream's scratch).  A batch of >= 64 commits
- * runs as two halves, one on `stream` and one on a library-owned stream joined to it by events
- * (the samplers of one half overlap the other half's core); the outputs are complete, as usual,
- * when `stream` has passed the call. */
+ * rg_jindo_commit_dev on that randomness (kept in the stream's scratch).  The batch runs as a DAG
+ * over `stream` and two library-owned streams of that caller stream joined to it by events (the
+ * COSAC sampler and the MLWE samplers beside TwinCDT, so each fills the others' tails); the
+ * outputs are complete, as usual, when `stream` has passed the call. */
 rg_status rg_jindo_commit_sampled_dev(const rg_jindo* j, size_t batch, const uint64_t* d_v, size_t nv,
                                       const rg_jindo_seeds* seeds, unsigned long long first_commit, uint64_t* d_incom,
                                       uint64_t* d_enc, uint64_t* d_mlwe, uint64_t* d_com, void* stream);

@@ -2914,8 +2914,8 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
 }
 
 // lastRow/mask (crypto/rand), then digits, then every Gaussian sample of the batch
-// Streams: st runs MustSetRandom, the digits and TwinCDT (cdt2); s_cos, once the digits are done
-// (event e_dig), the COSAC centres and cosac2; s_ml, once st reaches this call (event e_start),
+// Streams: st runs MustSetRandom, the digits, the COSAC centres and TwinCDT (cdt2); s_cos, once the
+// centres are done (event e_dig), cosac2; s_ml, once st reaches this call (event e_start),
 // the MLWE samplers, which need neither.  s_cos / s_ml may be st itself (one stream, no events).
 // The caller joins s_cos and s_ml back into st before it reads their outputs.
 static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, size_t nv, const rg_jindo_seeds* seeds,
@@ -2988,16 +2988,18 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
     a.cdt_jmax = S.cdt_jmax.as<int>();
     a.wq = sc->wq.as<int>();
     RG_HIP(hipMemsetAsync(a.wq, 0, 4 * sizeof(int), st));  // [0]: cdt2's chunks, [2..3]: cosac2's jobs (u64)
+    // the COSAC centres (small) ahead of cdt2 on st: launched on s_cos beside cdt2 they wait for
+    // cdt2's one-per-CU workgroups to finish (configs[4]: 6.9 ms), and cosac2 with them
+    const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
+    hipLaunchKernelGGL(cos_centre_kernel, dim3((unsigned)((ncos + kCentreWaves - 1) / kCentreWaves)),
+                       dim3(64 * kCentreWaves), 0, st, a);
+    RG_TRY(check_launch("jindo enc noise (COSAC centres)"));
     if (s_cos != st) {
       RG_HIP(hipEventRecord(e_dig, st));
       RG_HIP(hipStreamWaitEvent(s_cos, e_dig, 0));
     }
     hipLaunchKernelGGL(cdt2_noise_kernel, dim3(g), dim3(64 * kCdt2Waves), cdt2_dyn_lds(S.cdt_enc_size), st, a);
     RG_TRY(check_launch("jindo enc noise (TwinCDT)"));
-    const long long ncos = (long long)batch * (p.cols + p.rows);  // COSAC jobs
-    hipLaunchKernelGGL(cos_centre_kernel, dim3((unsigned)((ncos + kCentreWaves - 1) / kCentreWaves)),
-                       dim3(64 * kCentreWaves), 0, s_cos, a);
-    RG_TRY(check_launch("jindo enc noise (COSAC centres)"));
     const long long w2 = kCos2Threads / 64;
     const unsigned g2 = (unsigned)std::min<long long>((ncos + w2 - 1) / w2, 256);
     hipLaunchKernelGGL(cosac2_noise_kernel, dim3(g2), dim3(kCos2Threads), 0, s_cos, a);

@@ -238,6 +238,9 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
 #ifndef RG_NTT256_PLANES
 #define RG_NTT256_PLANES 2
 #endif
+#ifndef RG_NTT256_WL
+#define RG_NTT256_WL 0  // A/B knob: wave-private exchanges without workgroup barriers (below)
+#endif
 #ifndef RG_NTT256_WPE
 #define RG_NTT256_WPE 1  // amdgpu_waves_per_eu lower bound (A/B knob)
 #endif
@@ -324,14 +327,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
     }
   };
   // registers written at positions px(i) (phase pp) are read back at positions gx(i) (phase gp);
-  // pre: the LDS image may still be read by an earlier exchange (barrier first)
+  // pre: the LDS image may still be read by an earlier exchange (barrier first).
+  // Wave-private exchanges (RG_NTT256_WL): a ROW sub-transform is 32 lanes of one wave (s = tid >> 5)
+  // and every ROW position stays in its row s, so ROW exchanges never cross waves; COL's M <-> L
+  // (LOGC = 8) keeps x's top 3 bits = t >> 2, i.e. a wave's half of every column.  Those use only a
+  // compiler-level fence (a wave's LDS operations run in order); COL's H <-> M keeps its barriers,
+  // and so does COL at LOGC = 7 (N = 2^15), whose M pattern takes x's top bit from the register.
   auto xchg = [&](auto px, int pp, auto gx, int gp, bool pre) {
+    const bool wl = RG_NTT256_WL && (!COL || (LOGC == 8 && pp == ML && gp == ML));
+    auto sync = [&]() {
+      if (wl)
+        ntt_wave_fence();
+      else
+        __syncthreads();
+    };
 #pragma unroll
     for (int l0 = 0; l0 < 4; l0 += NPL) {
-      if (pre || l0 > 0) __syncthreads();
+      if (pre || l0 > 0) sync();
 #pragma unroll
       for (int i = 0; i < 8; ++i) put(i, px(i), pp, l0);
-      __syncthreads();
+      sync();
 #pragma unroll
       for (int i = 0; i < 8; ++i) get(i, gx(i), gp, l0);
     }

@@ -543,9 +543,12 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   }
 }
 
+#ifndef RG_NTT_LDS_PAD
+#define RG_NTT_LDS_PAD 0  // A/B knob: extra LDS words per workgroup (occupancy experiments)
+#endif
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP = false, int MINW = 1, int PROBE = 0>
 __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
-  __shared__ uint64_t lds[16 * 288];
+  __shared__ uint64_t lds[16 * 288 + RG_NTT_LDS_PAD];
   __shared__ ulonglong2 ltw[(COL || RP) && RG_NTT_LTW ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
   ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds, ltw);
 }

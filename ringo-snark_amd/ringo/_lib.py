@@ -7,8 +7,9 @@ import re
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # RINGO_LIB: another build of the same ABI (tools/: profiling variants, the experiments build)
 LIB_PATH = os.environ.get("RINGO_LIB") or os.path.join(_ROOT, "lib", "libringo.so")
-# the experiments build (ringo-snark_amd/Makefile): RINGO_* kernel switches and rg_set_probe honoured
-EXP_LIB_PATH = os.path.join(_ROOT, "lib", "libringo_exp.so")
+# the experiments build (ringo-snark_amd/Makefile): RINGO_* kernel switches and rg_set_probe honoured;
+# RINGO_EXP_LIB: an experiments-build variant (tools/var_build.sh exp_<name>)
+EXP_LIB_PATH = os.environ.get("RINGO_EXP_LIB") or os.path.join(_ROOT, "lib", "libringo_exp.so")
 HEADER = os.path.join(os.path.dirname(_ROOT), "include", "ringo.h")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)

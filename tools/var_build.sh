@@ -23,7 +23,9 @@ for f in "${tus[@]}"; do
     -I$R/include -I$C/csrc -c $T/$f -o $T/$b.o
   skip="$skip -e /$b.o"
 done
-objs=$(ls $C/build/*.o | grep -v -e knobs_env.o $skip)
+# a name starting with exp_ links the experiments build's knobs (RINGO_* switches, rg_set_probe)
+case $name in exp_*) drop=knobs.o;; *) drop=knobs_env.o;; esac
+objs=$(ls $C/build/*.o | grep -v -e "/$drop" $skip)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -Wl,-Bsymbolic -o $C/vlib/libringo_$name.so $objs $(for f in "${tus[@]}"; do echo $T/${f%.hip}.o; done)
 rm -rf $T
 echo built $C/vlib/libringo_$name.so
