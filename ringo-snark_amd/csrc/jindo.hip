@@ -1061,6 +1061,7 @@ struct RoundArgs {
   uint64_t* out;       // [npoly] at stride out_stride, dst.n limbs (+ zero rows up to out_rows)
   long long out_stride;
   int out_rows;
+  long long npoly;     // round256_kernel's polynomials (round_kernel: the grid)
 };
 
 __device__ __forceinline__ void mw_muladd(uint64_t* v, int nw, uint64_t m, uint64_t add) {
@@ -1181,6 +1182,158 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
   for (int k = tid; k < a.out_rows * d; k += blockDim.x) out[k] = (k / d < nd) ? poly(k / d)[k % d] : 0;
 }
 
+
+// Wave-per-polynomial round for d = 256 (every Jindo shape): one wave owns one polynomial, a
+// limb pair at a time in its two half-waves (lanes 0-31 limb l0, 32-63 limb l0 + 1), 8 points per
+// lane in registers.  The inverse and forward 256-point transforms run as rounds of 3 + 3 + 2
+// radix-2 stages (ntt64.hpp's ROW index algebra, lazy [0, 2q) Shoup butterflies) with wave-private
+// LDS exchanges and no workgroup barrier; the CRT step reads each coefficient's residues from the
+// wave's limb rows.  round_kernel (a workgroup per polynomial, a barrier per stage) does the same
+// arithmetic; results are the same canonical residues.
+constexpr int kRoundWaves = 4;
+template <int RK, int LO, int PAT, bool INV>
+__device__ __forceinline__ void wround(uint64_t (&e)[8], const ulonglong2* roots, const Q64& Q, uint32_t t) {
+  auto xof = [&](int rho) -> uint32_t {
+    if (PAT == 0) return t + 32u * rho;
+    if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
+    return 8u * t + rho;
+  };
+  constexpr int NPK = 1 << RK;
+#pragma unroll
+  for (int sp = 0; sp < RK; ++sp) {
+    const int bw = INV ? sp : RK - 1 - sp, b = LO + bw, k = 7 - b, half = 1 << bw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int grp = j / (NPK / 2), jj = j % (NPK / 2);
+      const int rho0 = grp * NPK + ((jj >> bw) << (bw + 1)) + (jj & (half - 1)), rho1 = rho0 + half;
+      const ulonglong2 w = roots[(1u << k) + (xof(rho0) >> (b + 1))];
+      if constexpr (INV)
+        inv_bfly_lazy<false>(e[rho0], e[rho1], w.x, w.y, Q);
+      else
+        fwd_bfly_lazy<false>(e[rho0], e[rho1], w.x, w.y, Q);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * kRoundWaves) void round256_kernel(RoundArgs a) {
+  // dynamic LDS: the limbs' tables (ns inverse, then nd forward; [l][256]), then per wave `rows`
+  // rows of 288 words: limb l's exchanges and its natural-order coefficients in row l
+  extern __shared__ ulonglong2 rtab[];
+  const int ns = a.src.n, nd = a.dst.n, rows = (std::max(ns, nd) + 1) & ~1;
+  for (int i = threadIdx.x; i < (ns + nd) * 256; i += blockDim.x)
+    rtab[i] = i < ns * 256 ? a.src.bwd[i] : a.dst.fwd[i - ns * 256];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* wl = reinterpret_cast<uint64_t*>(rtab + (ns + nd) * 256) + (size_t)wv * rows * 288;
+  const long long pid = (long long)blockIdx.x * kRoundWaves + wv;
+  if (pid >= a.npoly) return;
+  const uint64_t* in = a.in + pid * ns * 256;
+  // 1. IMForm, inverse NTT (Gentleman-Sande, bit-reversed -> natural), times 256^-1, per limb pair
+  for (int l0 = 0; l0 < ns; l0 += 2) {
+    const int limb = l0 + (int)hs, lc = limb < ns ? limb : l0;
+    const RnsPrime& P = a.src.p[lc];
+    const Q64 Q = make_q64(P.q);
+    const ulonglong2* roots = rtab + lc * 256;
+    const uint32_t row = 288u * (uint32_t)(l0 + (int)hs);
+    const uint32_t rH = row + t, rM = row + 36 * (t >> 2) + (t & 3), rL9 = row + 9 * t, rL8 = row + 8 * t + (t >> 2);
+    uint64_t e[8];
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = sh_mul(in[lc * 256 + t + 32 * y], P.rinv, P.rinv_sh, P.q);
+#pragma unroll
+    for (int y = 0; y < 8; ++y) wl[rH + 33 * y] = e[y];  // H -> L (pad x >> 5)
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) e[r] = wl[rL8 + r];
+    wround<2, 0, 2, true>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) wl[rL9 + r] = e[r];  // L -> M
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = wl[rM + 4 * y + (y >> 1)];
+    wround<3, 2, 1, true>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) wl[rM + 4 * y] = e[y];  // M -> H
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = wl[rH + 36 * y];
+    wround<3, 5, 0, true>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) wl[row + t + 32 * y] = sh_mul(e[y], P.ninv, P.ninv_sh, P.q);  // natural order
+    wave_lds_fence();
+  }
+  // 2. CRT per coefficient (4 per lane), floor shift, the destination residues in MForm
+  for (int i = 0; i < 4; ++i) {
+    const int k = (int)lane + 64 * i;
+    uint64_t r[kMaxQ];
+    for (int l = 0; l < ns; ++l) r[l] = wl[288 * l + k];
+    uint64_t mag[4];
+    const bool neg = crt_centred(a.crt, ns, r, mag);
+    bool lost = false;
+    int cut = a.cut;
+    while (cut > 0) {
+      const int sft = cut > 63 ? 63 : cut;
+      lost |= (mag[0] & ((1ull << sft) - 1)) != 0;
+      for (int w = 0; w < 4; ++w) mag[w] = (mag[w] >> sft) | (w + 1 < 4 ? mag[w + 1] << (64 - sft) : 0);
+      cut -= sft;
+    }
+    if (neg && lost) {
+      for (int w = 0; w < 4; ++w)
+        if (++mag[w]) break;
+    }
+    const bool zero = !(mag[0] | mag[1] | mag[2] | mag[3]);
+    for (int l = 0; l < nd; ++l) {
+      const RnsPrime& P = a.dst.p[l];
+      const uint64_t q = P.q;
+      uint64_t m = 0;
+      for (int w = 0; w < 4; ++w) m = mod_add(m, sh_mul(mag[w], a.dm.pw[l][w], a.dm.pw_sh[l][w], q), q);
+      if (neg && !zero) m = mod_neg(m, q);
+      r[l] = sh_mul(m, P.r64, P.r64_sh, q);
+    }
+    for (int l = 0; l < nd; ++l) wl[288 * l + k] = r[l];
+  }
+  wave_lds_fence();
+  // 3. forward NTT (Cooley-Tukey, natural -> bit-reversed) per destination limb pair, stored in H
+  uint64_t* out = a.out + pid * a.out_stride;
+  for (int l0 = 0; l0 < nd; l0 += 2) {
+    const int limb = l0 + (int)hs, lc = limb < nd ? limb : l0;
+    const Q64 Q = make_q64(a.dst.p[lc].q);
+    const ulonglong2* roots = rtab + (ns + lc) * 256;
+    const uint32_t row = 288u * (uint32_t)(l0 + (int)hs);
+    const uint32_t rH = row + t, rM = row + 36 * (t >> 2) + (t & 3), rL9 = row + 9 * t, rL8 = row + 8 * t + (t >> 2);
+    uint64_t e[8];
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = wl[288 * lc + t + 32 * y];
+    wave_lds_fence();
+    wround<3, 5, 0, false>(e, roots, Q, t);
+#pragma unroll
+    for (int y = 0; y < 8; ++y) wl[rH + 36 * y] = e[y];  // H -> M
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) e[y] = wl[rM + 4 * y];
+    wround<3, 2, 1, false>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < 8; ++y) wl[rM + 4 * y + (y >> 1)] = e[y];  // M -> L
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) e[r] = wl[rL9 + r];
+    wround<2, 0, 2, false>(e, roots, Q, t);
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) wl[rL8 + r] = canon(e[r], Q);  // L -> H, canonical
+    wave_lds_fence();
+    if (limb < nd) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) out[limb * 256 + t + 32 * y] = wl[rH + 33 * y];
+    }
+    wave_lds_fence();
+  }
+  for (int k = nd * 256 + (int)lane; k < a.out_rows * 256; k += 64) out[k] = 0;
+}
 
 // ------------------------------------------------------------------------------------------
 // 6. sampling: the randomness Prover.Commit draws (prover.go:65-139, encoder.go:149-183) on the
@@ -2687,6 +2840,28 @@ static rg_status on_device(const rg_jindo* J) {
 
 // The deterministic Ajtai core (prover.go:144-202) over a batch of NTT-domain openings:
 // inner MAC, rounding into Opening.InCommit, outer MAC and rounding into Commitment.Value.
+// CRT rounding of `npoly` polynomials: round256_kernel (a wave per polynomial) for d = 256 and
+// primes below 2^62 (its lazy butterflies need 2q < 2^63), round_kernel otherwise
+#ifndef RG_ROUND_WAVE
+#define RG_ROUND_WAVE 1  // A/B knob: 0 = round_kernel everywhere
+#endif
+static rg_status launch_round(RoundArgs ra, long long npoly, hipStream_t st) {
+  ra.npoly = npoly;
+  bool small = ra.d == 256;
+  for (int l = 0; l < ra.src.n; ++l) small = small && ra.src.p[l].q < (1ull << 62);
+  for (int l = 0; l < ra.dst.n; ++l) small = small && ra.dst.p[l].q < (1ull << 62);
+  if (RG_ROUND_WAVE && small) {
+    const int rows = (std::max(ra.src.n, ra.dst.n) + 1) & ~1;
+    const size_t lds = (size_t)(ra.src.n + ra.dst.n) * 256 * sizeof(ulonglong2) + (size_t)kRoundWaves * rows * 288 * 8;
+    hipLaunchKernelGGL(round256_kernel, dim3((unsigned)((npoly + kRoundWaves - 1) / kRoundWaves)), dim3(64 * kRoundWaves),
+                       lds, st, ra);
+  } else {
+    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256),
+                       (size_t)std::max(ra.src.n, ra.dst.n) * ra.d * 8, st, ra);
+  }
+  return check_launch("jindo round");
+}
+
 static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, const uint64_t* d_mlwe,
                              uint64_t* d_incom, uint64_t* d_com, rg_jindo_scratch* sc, hipStream_t st) {
   const rg_jindo_params& p = J->p;
@@ -2735,8 +2910,7 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   ra.out_rows = nqo;
   {
     const long long npoly = (long long)batch * (p.cols + 1) * p.in_msis;  // == batch * dcmp, same order
-    hipLaunchKernelGGL(round_kernel, dim3((unsigned)npoly), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
-    RG_TRY(check_launch("jindo round(in)"));
+    RG_TRY(launch_round(ra, npoly, st));
   }
   // 5. outer MAC + round -> Commitment.Value (ringQ-shaped rows, rows >= nqo zero)
   MacArgs mo;
@@ -2767,7 +2941,7 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   ro.out = d_com;
   ro.out_stride = (long long)nq * d;
   ro.out_rows = nq;
-  hipLaunchKernelGGL(round_kernel, dim3((unsigned)(batch * p.out_msis)), dim3(256), (size_t)nqo * d * 8, st, ro);
+  RG_TRY(launch_round(ro, (long long)batch * p.out_msis, st));
   RG_TRY(check_launch("jindo round(out)"));
   return RG_OK;
 }
@@ -3402,8 +3576,7 @@ rg_status rg_jindo_verify_dev(const rg_jindo* J, size_t batch, const uint64_t* d
     ra.out = lift.as<uint64_t>();
     ra.out_stride = pq;
     ra.out_rows = nq;
-    hipLaunchKernelGGL(round_kernel, dim3((unsigned)p.dcmp), dim3(256), (size_t)std::max(nq, nqo) * d * 8, st, ra);
-    RG_TRY(check_launch("jindo verify lift"));
+    RG_TRY(launch_round(ra, p.dcmp, st));
   }
   {
     MacArgs m = dot_args(J->rq, nq, d, p.in_msis, p.cols, d_chals, lift.as<uint64_t>(), pq, (long long)p.in_msis * pq,

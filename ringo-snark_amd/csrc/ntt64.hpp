@@ -266,10 +266,15 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 // LDS exchanges) of the same launch, timed by bench.py through rg_set_probe
 // LTW: the L round (PAT 2) reads its twiddles from the tile's LDS copy `ltw` (192 entries staged
 // by ntt16_tile: COL tw[64, 256), RP the row's lane-ordered copy) instead of per-lane global loads
-template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
+// PIPE (ntt16_pipe): no vector-memory loads at all (an LDS-DMA of the next tile is in flight, and a
+// vector load's vmcnt wait would drain it): the H round's uniform twiddles by scalar loads through
+// the constant address space, the M round's from the workgroup's LDS copy `mtw` (56 entries:
+// mtw[2^k - 8 + j] = tw[2^(G0+k) + (hi << k) + j], k = 3..5), the L round's from `ltw`.
+template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE, bool PIPE = false>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
-                                            uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr) {
-  constexpr bool LTW = PAT == 2 && (COL || RP) && RG_NTT_LTW;
+                                            uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr,
+                                            const ulonglong2* mtw = nullptr) {
+  constexpr bool LTW = PAT == 2 && (COL || RP) && (RG_NTT_LTW || PIPE);
   constexpr int G0 = COL ? 0 : 8;
   // twiddle index independent of the lane: the H round of COL / RP tiles.  (The M round of COL
   // tiles is wave-uniform too, x >> (b + 1) depending on t >> 2 = tid >> 6 only, but scalar loads
@@ -306,10 +311,20 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
       if constexpr ((PROBE & 1) != 0) {
         w[j] = a.w1n + (xof(rho0) >> (b + 1)) + hi;
         wp[j] = a.w1n_p;
+      } else if constexpr (UNIFORM && PIPE) {
+        const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
+        const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
+        typedef const __attribute__((address_space(4))) uint64_t* cptr;
+        w[j] = ((cptr)a.tw)[2 * iu];
+        wp[j] = ((cptr)a.tw)[2 * iu + 1];
       } else if constexpr (UNIFORM) {
         const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
         const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
         const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[iu];
+        w[j] = v.x;
+        wp[j] = v.y;
+      } else if constexpr (PIPE && PAT == 1) {
+        const ulonglong2 v = mtw[(1u << k) - 8u + (xof(rho0) >> (b + 1))];
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (LTW && COL) {
@@ -383,8 +398,16 @@ __device__ __forceinline__ void ntt_wave_fence() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
-template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0>
-__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw) {
+// raw workgroup barrier: waits for the wave's LDS operations only (never vmcnt, so an LDS-DMA in
+// flight survives it); the asm's memory clobber keeps LDS accesses on their side of it
+__device__ __forceinline__ void ntt_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// PIPE: the tile is already in `lds` (ntt16_pipe's LDS-DMA, in the layout each pass's first LDS
+// exchange uses: COL the transposed image, ROW rows [s][x] at pitch 288); each lane reads its first
+// round's points from there instead of HBM, and the barriers are ntt_lds_barrier
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0, bool PIPE = false>
+__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw,
+                                           const ulonglong2* mtw = nullptr) {
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
@@ -401,11 +424,15 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
   constexpr bool WL = (RG_NTT_WL & (COL ? 2 : 1)) != 0;
-  constexpr bool LTW = (COL || RP) && RG_NTT_LTW && (PROBE & 1) == 0;
+  constexpr bool LTW = (COL || RP) && (RG_NTT_LTW || PIPE) && (PROBE & 1) == 0;
+  auto bar = [&]() {
+    if constexpr (PIPE) ntt_lds_barrier();
+    else __syncthreads();
+  };
   // an exchange inside one wave's LDS block / one that crosses waves
   auto wsync = [&]() {
     if constexpr (WL) ntt_wave_fence();
-    else __syncthreads();
+    else bar();
   };
   if constexpr (RG_NTT_STAGGER != 0) {  // first-generation workgroups of a CU start out of phase
     if (tile < 1024u) {
@@ -420,15 +447,28 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   // tile's data (its wait then covers this load only) and written to LDS after they are issued
   uint64_t ltw_word = 0;
   const uint32_t ltw_base = COL ? 64u : 65536u + hi * 192u;
-  if constexpr (LTW && !WL) {
+  if constexpr (LTW && !WL && !PIPE) {
     if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
   }
-  if constexpr (LTW && WL) {
+  if constexpr (LTW && WL && !PIPE) {
     if (tid < 384u) ltw_word = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
   }
+  (void)ltw_base;
+  (void)ltw_word;
   // ---- global load (RG_NTT_PRIO: the wave issues its tile loads at raised priority)
   if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(3);
-  if constexpr ((PROBE & 4) != 0) {
+  if constexpr (PIPE) {
+    if constexpr (COL && !INV) {  // H: the image position 16 x + s + 16 (x >> 3) of x = t + 32 y
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[16 * t + s + 16 * (t >> 3) + 576 * y];
+    } else if constexpr (COL) {  // L: x = 8 t + r
+#pragma unroll
+      for (int r = 0; r < 8; ++r) e[r] = lds[144 * t + s + 16 * r];
+    } else {  // rows [s][x], H: x = t + 32 y
+#pragma unroll
+      for (int y = 0; y < 8; ++y) e[y] = lds[288 * s + t + 32 * y];
+    }
+  } else if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = (uint64_t)(tid * 0x9E3779B9u + tile * 8u + (uint32_t)y);
   } else if constexpr (COL) {
@@ -448,7 +488,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   }
   if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(0);
   if constexpr (RG_NTT_PRIO == 2) __builtin_amdgcn_s_setprio(2);  // 2: butterflies at raised priority
-  if constexpr (LTW && WL) {
+  if constexpr (LTW && WL && !PIPE) {
     if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = ltw_word;
     // COL forward reads ltw only after its H -> M barrier
     if constexpr (!COL || INV) __syncthreads();
@@ -466,15 +506,15 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t rH = 288 * s + t, rM = 288 * s + 36 * (t >> 2) + (t & 3), rL9 = 288 * s + 9 * t,
                  rL8 = 288 * s + 8 * t + (t >> 2);
   if constexpr (!INV) {
-    ntt16_round<3, 5, 0, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 5, 0, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t);
     // exchange H -> M (COL: across waves)
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bH + 576 * y : rH + 36 * y] = e[y];
-    if constexpr (COL) __syncthreads();
+    if constexpr (COL) bar();
     else wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y];
-    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, nullptr, mtw);
     wsync();
     // exchange M -> L
 #pragma unroll
@@ -482,7 +522,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     wsync();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[COL ? bL + 16 * r : rL9 + r];
-    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
+    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, ltw);
     if (CANON) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
@@ -509,24 +549,24 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
       for (int r = 0; r < 8; ++r) e[r] = lds[rL8 + r];
       wsync();
     }
-    if constexpr (COL && LTW && !WL) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
-    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
+    if constexpr (COL && LTW && !WL && !PIPE) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
+    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, ltw);
     // exchange L -> M
 #pragma unroll
     for (int r = 0; r < 8; ++r) lds[COL ? bL + 16 * r : rL9 + r] = e[r];
     wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)];
-    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, nullptr, mtw);
     wsync();
     // exchange M -> H (COL: across waves)
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y] = e[y];
-    if constexpr (COL) __syncthreads();
+    if constexpr (COL) bar();
     else wsync();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bH + 576 * y : rH + 36 * y];
-    ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t);
     if (CANON) {
 #pragma unroll
       for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
@@ -551,6 +591,77 @@ __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
   __shared__ uint64_t lds[16 * 288 + RG_NTT_LDS_PAD];
   __shared__ ulonglong2 ltw[(COL || RP) && RG_NTT_LTW ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
   ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds, ltw);
+}
+
+// ----------------------------------------------------------------------------------------
+// Pipelined pass: persistent workgroups (2 per CU, 4 waves/SIMD), each walking tiles at the grid's
+// stride with two LDS images.  While tile k is transformed in image k & 1, tile k + 1 streams
+// from HBM into the other image by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no vmcnt wait
+// until the next tile), so the load latency that the one-tile-per-workgroup pass hides only with
+// 8 resident waves is hidden by the prefetch instead.  The DMA writes each pass's first exchange
+// layout directly: COL the transposed image (8-row blocks of 1 KiB at 1152-B pitch), ROW rows of
+// 2 KiB at the 288-word pitch.  The twiddles a workgroup needs are staged once: its tiles share
+// them (COL: every tile; ROW with RP and a grid that is a multiple of 256: tile & 255, the row, is
+// the same for every tile of a workgroup).  Results equal ntt16_pass's (same rounds, same images).
+__device__ __forceinline__ void ntt_glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+constexpr int kPipeImg = 16 * 288;  // u64 words per image (36 KiB)
+template <bool INV, bool COL, bool SCALE, bool CANON>
+__global__ __launch_bounds__(512, 1) void ntt16_pipe(Ntt64Args a, uint32_t ntiles) {
+  __shared__ uint64_t img[2 * kPipeImg];
+  __shared__ ulonglong2 ltw[192];
+  __shared__ ulonglong2 mtw[56];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t tile = blockIdx.x;
+  {  // the workgroup's twiddles (ntt16_round's PIPE sources)
+    const uint32_t hi = COL ? 0u : (tile & 255u);
+    const uint64_t* tw = reinterpret_cast<const uint64_t*>(a.tw);
+    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = tw[2ull * (COL ? 64u : 65536u + hi * 192u) + tid];
+    if (tid < 112u) {
+      const uint32_t j = tid >> 1;  // mtw[2^k - 8 + i] = tw[2^(G0+k) + (hi << k) + i], k = 3..5
+      const uint32_t k = j < 8u ? 3u : j < 24u ? 4u : 5u;
+      const uint32_t src = (1u << ((COL ? 0u : 8u) + k)) + (hi << k) + (j + 8u - (1u << k));
+      reinterpret_cast<uint64_t*>(mtw)[tid] = tw[2ull * src + (tid & 1u)];
+    }
+  }
+  const uint32_t img_lds = (uint32_t)(uintptr_t)img;
+  // tile -> LDS-DMA: 32 chunks of 1 KiB (64 lanes x 16 B), 4 per wave
+  auto dma = [&](uint32_t tl, uint32_t buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t c = w + 8u * (uint32_t)i;
+      size_t src;
+      uint32_t dst;  // bytes
+      if constexpr (COL) {  // rows 8c .. 8c + 7 of 16 columns: lane -> row 8c + lane / 8, 2 columns
+        src = ((size_t)(tl >> 4) << 16) + ((tl & 15u) << 4) + (size_t)(8u * c + (lane >> 3)) * 256u + 2u * (lane & 7u);
+        dst = c * 1152u;
+      } else {  // half h of row (tl & 255) of polynomial 16 (tl >> 8) + s
+        const uint32_t sr = c >> 1, h = c & 1u;
+        src = ((size_t)(16u * (tl >> 8) + sr) << 16) + ((tl & 255u) << 8) + 128u * h + 2u * lane;
+        dst = (288u * sr + 128u * h) * 8u;
+      }
+      ntt_glds16(a.in + src, img_lds + buf * (uint32_t)(kPipeImg * 8) + dst);
+    }
+  };
+  if (tile < ntiles) dma(tile, 0);
+  for (uint32_t k = 0; tile < ntiles; ++k, tile += gridDim.x) {
+    // tile k landed (every wave's DMA, then the barrier); the other image is free (tile k - 1 done)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const uint32_t nt = tile + gridDim.x;
+    if (nt < ntiles) dma(nt, (k + 1u) & 1u);
+    ntt16_tile<INV, COL, SCALE, CANON, !COL, 0, true>(a, tile, img + (k & 1u) * kPipeImg, ltw, mtw);
+  }
 }
 
 #endif  // __HIPCC__
