@@ -970,12 +970,10 @@ __global__ __launch_bounds__(256 * JG, 1) void mac3h_kernel(Mac3Args a) {
   }
 }
 
-// J padded to the instantiated widths
-#ifndef RG_MAC3_JP10
-#define RG_MAC3_JP10 0  // 0: J = 9..10 padded to JP = 12 (1,024-thread mac3h<12,4>) instead of mac3h<10,2>
-#endif
+// J padded to the instantiated widths (J = 9..10 padded to 12: the 1,024-thread mac3h<12,4> measured
+// faster than a 512-thread mac3h<10,2>, whose 110 KiB ring capped it at 2 waves/SIMD)
 static int mac3_jp(int J) {
-  static const int w[] = {4, 6, 8, RG_MAC3_JP10 ? 10 : 12, 12, 16};
+  static const int w[] = {4, 6, 8, 12, 12, 16};
   for (int x : w)
     if (J <= x) return x;
   return 0;
@@ -1405,18 +1403,6 @@ __device__ __forceinline__ double enc_centre(const SampleArgs& a, const uint32_t
 // TwinCDT tables above kCdtLdsMaxSize entries: fields with exp >= 128, or caller stddevs far above
 // NewParameters').  The round-2 kernels that covered them (enc_noise_kernel, cdt_noise_kernel +
 // cdt_tail_kernel) are tools/experiments/legacy_samplers.patch.
-// profiling variants' stand-in keystream (never in a production build)
-__device__ __forceinline__ uint64_t var_mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-#ifndef RG_VAR
-#define RG_VAR 0  // profiling variants (tools/variants.sh): 1 no tail, 2 no AES, 4 no search, 8 no AES (COSAC),
-                  // 16 no AES in cosac2, 32 no AES in cdt2 (keystream replaced by a SplitMix64 hash),
-                  // 64 cosac2 without libm exp / log (cheap stand-ins: cost of the rare branches)
-#endif
 #pragma clang fp contract(off)
 constexpr int kCdtLdsMaxSize = 96;  // tables' high words + guide in LDS when size <= 96 (<= 145 KiB
                                     // per workgroup with the 64 KiB AES table)
@@ -1562,8 +1548,6 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   __syncthreads();
   const JShape& S = a.s;
   const long long npoly = a.batch * (S.cols + 1) * S.rows;
-  const long long nw = (long long)gridDim.x * kCdt2Waves;
-  (void)nw;
   const double norm = sqrt(2.0 * M_PI) * C.sigma;
   const double two_s2 = 2.0 * C.sigma * C.sigma;
   const LdsKey key{keyl};
@@ -1573,20 +1557,12 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
   const dconst_ptr dlt = (dconst_ptr)a.delta;
   int i0 = 0;  // first nonzero deltaInv
   while (i0 < S.exp && dlt[i0] == 0.0) ++i0;
-#ifndef RG_CDT2_QUEUE
-#define RG_CDT2_QUEUE 1  // 0: the static chunk assignment (chunk w, w + waves, ...), for A/B
-#endif
   // chunks from a counter: a wave that drew cheap polynomials (COSAC hand-offs, skipped ones)
   // takes more, so the workgroups -- one per CU, whose last wave holds its CU -- end together
-  for (long long it = 0;; ++it) {
-    long long p0;
-    if constexpr (RG_CDT2_QUEUE) {
-      int ch = 0;
-      if (lane == 0) ch = atomicAdd(a.wq, 1);
-      p0 = (long long)__builtin_amdgcn_readlane(ch, 0) * kCdtChunk;
-    } else {
-      p0 = (((long long)blockIdx.x * kCdt2Waves + wl) + it * nw) * kCdtChunk;
-    }
+  for (;;) {
+    int ch = 0;
+    if (lane == 0) ch = atomicAdd(a.wq, 1);
+    const long long p0 = (long long)__builtin_amdgcn_readlane(ch, 0) * kCdtChunk;
     if (p0 >= npoly) break;
     const long long p1 = p0 + kCdtChunk < npoly ? p0 + kCdtChunk : npoly;
     int row = (int)(p0 % S.rows), col = (int)((p0 / S.rows) % (S.cols + 1));
@@ -1615,11 +1591,7 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
       const unsigned long long gpoly =
           a.first_commit * (unsigned long long)(S.cols + 1) * S.rows + (unsigned long long)poly;
       uint64_t u[4];
-#if RG_VAR & 32
-      for (int h = 0; h < 4; ++h) u[h] = var_mix64(gpoly * 0x9E3779B97F4A7C15ull + 4u * lane + h);
-#else
       ks_words_x2(key, gpoly, (uint64_t)(2 * lane), (uint64_t)(2 * lane + 1), lds, u);
-#endif
       // TwinCDTGaussianSampler.Sample (twin_cdt.go:77-111).  Fast path: the guide bucket of u's
       // top byte in table c0 holds <= 3 entries and none shares u's high word, so the lower bound
       // is lo + #(entries below u) with no equality (three LDS word compares); and v0 <= jmax[c0],
@@ -1677,9 +1649,6 @@ __global__ __launch_bounds__(64 * kCdt2Waves) void cdt2_noise_kernel(SampleArgs 
             }
           }
       }
-#if RG_VAR & 1
-      pend = 0;
-#endif
       for (;;) {  // the exact sums (p within ~1e-12 of the cdf), one sample at a time across the wave
         const uint64_t any = __ballot(pend != 0);
         if (!any) break;
@@ -1763,13 +1732,6 @@ struct Cos2Lane {
 //          (1 + 2^-50) <= arg (the product form of the quotient, its rounding covered by the
 //          2^-50) and exp(arg) >= 1 + arg (exp within an ulp, covered by the 2^-48); else the
 //          reference's division and exp decide.
-#if RG_VAR & 64
-#define RG_COS_EXP(x) (1.0 + (x))
-#define RG_COS_LOG(x) ((x) - 1.0)
-#else
-#define RG_COS_EXP(x) exp(x)
-#define RG_COS_LOG(x) log(x)
-#endif
 template <class Z>
 __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, const double* sdv, long long* en) {
   const double rn = 3.442619855899;
@@ -1810,7 +1772,7 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
     if (!acc) {
       const double ap = -D * sdv[4 * code + 1] * (1.0 + 8.881784197001252e-16);  // a' <= arg < 0
       acc = fw < (1.0 + ap) * 0.99999999999999644729;
-      if (!acc) acc = fw < RG_COS_EXP(-D / (2.0 * sdv[4 * code] * sdv[4 * code]));
+      if (!acc) acc = fw < exp(-D / (2.0 * sdv[4 * code] * sdv[4 * code]));
     }
     if (acc) {
       en[L.oi] = (long long)L.y_round + (long long)L.c_int;
@@ -1822,7 +1784,7 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
     nst = kCoNorm;
     if (fw < sdv[4 * code + 3]) {  // r < 1 / lead: the reference's exp comparison decides
       const double sd = sdv[4 * code];
-      if (fw < RG_COS_EXP(-(L.c_frac * L.c_frac) / (2.0 * sd * sd)) / sdv[4 * code + 2]) {
+      if (fw < exp(-(L.c_frac * L.c_frac) / (2.0 * sd * sd)) / sdv[4 * code + 2]) {
         en[L.oi] = (long long)L.c_int;
         done = true;
       }
@@ -1830,14 +1792,14 @@ __device__ __forceinline__ bool cos2_step(Cos2Lane& L, uint64_t w, const Z& Zg, 
   } else if (st == kCoWedge) {  // gaussian_rounded.go:109-113
     const int zi = (L.st >> 8) & 127;
     const double f0 = Zg.fn[zi - 1], f1 = Zg.fn[zi];
-    if (fw * (f0 - f1) < RG_COS_EXP(-0.5 * L.t * L.t) - f1) {
+    if (fw * (f0 - f1) < exp(-0.5 * L.t * L.t) - f1) {
       nf = L.t;
       have_nf = true;
     } else {
       nst = kCoNorm;
     }
   } else {  // kCoTailU / kCoTailV, gaussian_rounded.go:94-101
-    const double lg = -RG_COS_LOG(fw);
+    const double lg = -log(fw);
     if (st == kCoTailU) {
       L.t = lg * (1.0 / rn);
       nst = kCoTailV;
@@ -1881,22 +1843,16 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
   __syncthreads();
   const ZigDev Z{zig, reinterpret_cast<const double*>(zig + 128), reinterpret_cast<const double*>(zig + 256)};
   const JShape& S = a.s;
-  const long long nwaves = (long long)gridDim.x * (kCos2Threads / 64);
-  const long long wid = (long long)blockIdx.x * (kCos2Threads / 64) + (threadIdx.x >> 6);
   const int per = S.cols + S.rows;
   const long long njobs = a.batch * per;
-  const long long myjobs = njobs > wid ? (njobs - wid + nwaves - 1) / nwaves : 0;
   constexpr int NG = 256 / kCosGroup;  // groups per polynomial
-#ifndef RG_COS2_CHUNKS
-#define RG_COS2_CHUNKS 1  // 0: each wave's fixed queue (jobs wid, wid + waves, ...), for A/B
-#endif
-  // RG_COS2_CHUNKS: a wave's queue is refilled kCos2Chunk jobs at a time from one counter (one
-  // atomic per chunk), so waves whose groups drew few words take more jobs; results do not depend
-  // on which wave draws a group
+  // a wave's queue is refilled kCos2Chunk jobs at a time from one counter (one atomic per chunk),
+  // so waves whose groups drew few words take more jobs; results do not depend on which wave draws
+  // a group
   constexpr int kCos2Chunk = 64 / NG;  // jobs per refill: one group per lane of the wave
-  long long total = RG_COS2_CHUNKS ? 0 : myjobs * NG;  // this wave's queue of groups
-  long long job0 = 0;                                 // RG_COS2_CHUNKS: the chunk's first job
-  bool drained = false;                               // RG_COS2_CHUNKS: the counter passed njobs
+  long long total = 0;   // groups in the wave's current chunk
+  long long job0 = 0;    // the chunk's first job
+  bool drained = false;  // the counter passed njobs
   unsigned long long* cq = reinterpret_cast<unsigned long long*>(a.wq + 2);
   const unsigned long long pbg = a.first_commit * (unsigned long long)(S.cols + 1) * S.rows * (unsigned long long)NG;
   auto mb = [](uint64_t m) {
@@ -1924,7 +1880,7 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
         const uint64_t need = __ballot(L.g < 0);
         if (!need) break;
         if (next >= total) {
-          if (!RG_COS2_CHUNKS || drained) break;
+          if (drained) break;
           unsigned long long base = 0;
           if ((threadIdx.x & 63) == 0) base = atomicAdd(cq, (unsigned long long)kCos2Chunk);
           job0 = (long long)(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), 0) << 32) |
@@ -1939,7 +1895,7 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
         const int rank = mb(need);
         if (L.g < 0 && next + rank < total) {
           const long long g = next + rank;
-          const long long job = RG_COS2_CHUNKS ? job0 + g / NG : wid + (g / NG) * nwaves;
+          const long long job = job0 + g / NG;
           const long long b = job / per;
           const int j = (int)(job % per);
           const int col = j < S.cols ? j : S.cols, row = j < S.cols ? 0 : j - S.cols;
@@ -1964,12 +1920,7 @@ __global__ __launch_bounds__(kCos2Threads, 1) void cosac2_noise_kernel(SampleArg
         const LdsKey k{keys + s * kCos2KeyStride};
         if (p < 1024) {
           uint64_t w1;
-#if RG_VAR & 16
-          w = var_mix64(inst * 0x9E3779B97F4A7C15ull + 2u * p + 1315423911u * s);
-          w1 = var_mix64(w);
-#else
           ks_words(k, inst, p / 2, lds, w, w1);
-#endif
           if (s)
             L.spare[1] = w1;
           else
@@ -2841,16 +2792,14 @@ static rg_status on_device(const rg_jindo* J) {
 // The deterministic Ajtai core (prover.go:144-202) over a batch of NTT-domain openings:
 // inner MAC, rounding into Opening.InCommit, outer MAC and rounding into Commitment.Value.
 // CRT rounding of `npoly` polynomials: round256_kernel (a wave per polynomial) for d = 256 and
-// primes below 2^62 (its lazy butterflies need 2q < 2^63), round_kernel otherwise
-#ifndef RG_ROUND_WAVE
-#define RG_ROUND_WAVE 1  // A/B knob: 0 = round_kernel everywhere
-#endif
+// primes below 2^62 (its lazy butterflies need 2q < 2^63), round_kernel otherwise.  round256
+// against round_kernel at configs[4]: 429 vs 513 us per launch (profiles/r05s_round_wave_ab.txt)
 static rg_status launch_round(RoundArgs ra, long long npoly, hipStream_t st) {
   ra.npoly = npoly;
   bool small = ra.d == 256;
   for (int l = 0; l < ra.src.n; ++l) small = small && ra.src.p[l].q < (1ull << 62);
   for (int l = 0; l < ra.dst.n; ++l) small = small && ra.dst.p[l].q < (1ull << 62);
-  if (RG_ROUND_WAVE && small) {
+  if (small) {
     const int rows = (std::max(ra.src.n, ra.dst.n) + 1) & ~1;
     const size_t lds = (size_t)(ra.src.n + ra.dst.n) * 256 * sizeof(ulonglong2) + (size_t)kRoundWaves * rows * 288 * 8;
     hipLaunchKernelGGL(round256_kernel, dim3((unsigned)((npoly + kRoundWaves - 1) / kRoundWaves)), dim3(64 * kRoundWaves),
@@ -3069,10 +3018,7 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.mask = mask;
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
   const dim3 ug((unsigned)std::min<long long>((a.total + 511) / 512, 1024));
-#ifndef RG_UNI_WHOLE
-#define RG_UNI_WHOLE 1  // 0: every draw on uniform_elems_kernel (A/B)
-#endif
-  if constexpr (L % 2 == 0 && RG_UNI_WHOLE) {
+  if constexpr (L % 2 == 0) {
     if (a.kbytes == 8 * L) {  // whole words: the common draws, then the (practically never) long ones
       const char* kt = knob(Knob::JindoUniTries);  // experiments build: cap the tries (fix-up test)
       const int tries = std::max(0, std::min(1024 / L, kt ? atoi(kt) : 1024 / L));

@@ -38,13 +38,9 @@ namespace rg {
 
 typedef int mfma_v4i __attribute__((ext_vector_type(4)));
 
-#ifndef RG_MFMA_STAGES
-#define RG_MFMA_STAGES 4
-#endif
-#ifndef RG_MFMA_LK
-#define RG_MFMA_LK 16  // lk per workgroup: 16 (1024 threads, one 128-B line) or 8 (512 threads, 2 per CU: measured 30% slower)
-#endif
-constexpr int kMfmaStages = RG_MFMA_STAGES;  // LDS ring depth
+constexpr int kMfmaStages = 4;  // LDS ring depth (3 / 4 / 5 measured within 1%, round 4)
+constexpr int kMfmaLk = 16;     // lk per workgroup: 16 (1024 threads, one 128-B line); 8 (512 threads,
+                                // 2 per CU) measured 30% slower
 
 __device__ __forceinline__ void mfma_glds16(const void* gsrc, uint32_t lds_dst) {
   uint32_t keep;
@@ -277,7 +273,7 @@ rg_status launch_mac_mfma(const MfmaMacArgs& args, int NB, hipStream_t st) {
     set_last_error("mac_mfma: shape outside the kernel's assumptions");
     return RG_ERR_INVALID;
   }
-  constexpr int LK = RG_MFMA_LK;
+  constexpr int LK = kMfmaLk;
   const long long blocks = (a.per_col / LK) * ((a.ncols + 15) / 16);
   const dim3 g((unsigned)blocks), b(64 * LK);
   switch (NB) {

@@ -133,7 +133,7 @@ __device__ __forceinline__ void canon256(uint32_t (&x)[8], const uint32_t (&q)[8
 }
 
 // Butterfly bodies.  Inlined: the tile is ~18K instructions, but the four independent
-// butterflies of a stage interleave; out of line (RG_NTT256_OUTLINE, 2.2K-instruction kernels)
+// butterflies of a stage interleave; out of line (__noinline__, 2.2K-instruction kernels) they
 // measured 1.5x slower (the calls serialise the butterflies).
 struct D8 {
   uint32_t d[8];
@@ -141,11 +141,7 @@ struct D8 {
 struct D16 {
   D8 x, y;
 };
-#ifdef RG_NTT256_OUTLINE
-#define RG_NTT256_BFLY __device__ __noinline__
-#else
 #define RG_NTT256_BFLY __device__ __forceinline__
-#endif
 RG_NTT256_BFLY D16 bfly_fwd256(D8 x, D8 y, D8 w, const Ntt256Args* a) {
   uint32_t tt[8];
   D16 r;
@@ -232,31 +228,24 @@ __device__ __forceinline__ void ntt256_round(const Ntt256Args& a, __amdgpu_buffe
 //   COL: pitch 296, pad (x >> 3) for every exchange; ROW: pitch 288, pads 4(x>>5) (H<->M),
 //   (x>>3) (M<->L), (x>>5) (L<->H) -- conflict-free for ds_*_b64 half-wave groups (checked by
 //   enumeration, tools/nttlab/banks.py).
-// An exchange moves the 4 limb planes through an LDS image of RG_NTT256_PLANES planes: with 2,
+// An exchange moves the 4 limb planes through an LDS image of kNtt256Planes planes: with 2,
 // two rounds of (put, barrier, get) of 2 planes each, so a 128-thread workgroup holds 18.9 KiB
 // instead of 37.9 KiB and occupancy is set by VGPRs (3-4 waves/SIMD), not LDS (2 waves/SIMD).
-#ifndef RG_NTT256_PLANES
-#define RG_NTT256_PLANES 2
-#endif
-#ifndef RG_NTT256_WL
-#define RG_NTT256_WL 0  // A/B knob: wave-private exchanges without workgroup barriers (below)
-#endif
-#ifndef RG_NTT256_WPE
-#define RG_NTT256_WPE 1  // amdgpu_waves_per_eu lower bound (A/B knob)
-#endif
+// (amdgpu_waves_per_eu(4), a 128-VGPR cap, spilled 1-26 VGPRs and measured 3% slower: round 2)
+constexpr int kNtt256Planes = 2;
 // LOGN = 16 (COL and ROW both 8-stage passes) or 15 (COL: 7 stages on 256 columns of 128 points,
 // 8 of them per tile; ROW: 8 stages on 128 rows of 256 points), as ntt.hip plans them.
 // PROBE (experiments build only, rg_set_probe(5); production = 0): 1 = no HBM data movement,
 // the tile synthesised in registers and the result kept live by a store that never fires, so the
 // same launch times the butterflies, twiddle loads and LDS exchanges alone.
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int LOGN = 16, int PROBE = 0>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_WPE))) void ntt256_pass(Ntt256Args a) {
+__global__ __launch_bounds__(128) void ntt256_pass(Ntt256Args a) {
   static_assert(LOGN == 15 || LOGN == 16, "ntt256_pass: N = 2^15 or 2^16");
   constexpr int LOGC = COL ? LOGN - 8 : 8;        // bits of a sub-transform
   constexpr uint32_t CPT = COL ? (1024u >> LOGC) : 4u;  // sub-transforms per tile
   constexpr int PITCH = COL ? (LOGC == 8 ? 296 : 148) : 288, PLANE = (int)CPT * PITCH;
-  constexpr int NPL = RG_NTT256_PLANES;  // limb planes per LDS round (4 or 2)
-  static_assert(NPL == 4 || NPL == 2, "RG_NTT256_PLANES");
+  constexpr int NPL = kNtt256Planes;  // limb planes per LDS round (4 or 2)
+  static_assert(NPL == 4 || NPL == 2, "kNtt256Planes");
   constexpr uint32_t R = 1u << (LOGN - 8);  // ROW: rows per polynomial; COL: tiles per polynomial x CPT / 256
   __shared__ uint64_t lds[NPL * PLANE];
   const uint32_t tid = threadIdx.x;
@@ -327,26 +316,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RG_NTT256_W
     }
   };
   // registers written at positions px(i) (phase pp) are read back at positions gx(i) (phase gp);
-  // pre: the LDS image may still be read by an earlier exchange (barrier first).
-  // Wave-private exchanges (RG_NTT256_WL): a ROW sub-transform is 32 lanes of one wave (s = tid >> 5)
-  // and every ROW position stays in its row s, so ROW exchanges never cross waves; COL's M <-> L
-  // (LOGC = 8) keeps x's top 3 bits = t >> 2, i.e. a wave's half of every column.  Those use only a
-  // compiler-level fence (a wave's LDS operations run in order); COL's H <-> M keeps its barriers,
-  // and so does COL at LOGC = 7 (N = 2^15), whose M pattern takes x's top bit from the register.
+  // pre: the LDS image may still be read by an earlier exchange (barrier first)
   auto xchg = [&](auto px, int pp, auto gx, int gp, bool pre) {
-    const bool wl = RG_NTT256_WL && (!COL || (LOGC == 8 && pp == ML && gp == ML));
-    auto sync = [&]() {
-      if (wl)
-        ntt_wave_fence();
-      else
-        __syncthreads();
-    };
 #pragma unroll
     for (int l0 = 0; l0 < 4; l0 += NPL) {
-      if (pre || l0 > 0) sync();
+      if (pre || l0 > 0) __syncthreads();
 #pragma unroll
       for (int i = 0; i < 8; ++i) put(i, px(i), pp, l0);
-      sync();
+      __syncthreads();
 #pragma unroll
       for (int i = 0; i < 8; ++i) get(i, gx(i), gp, l0);
     }

@@ -236,27 +236,20 @@ typedef unsigned int rg_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_buf(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
-#ifndef RG_NTT_AUX
-#define RG_NTT_AUX 2  // cache policy of the transform's data loads / stores: nt (measured -3% per step vs 0, sc1 no better)
-#endif
-#ifndef RG_NTT_LTW
-#define RG_NTT_LTW 1  // L-round twiddles staged in LDS per tile (COL, RP); 0 = per-lane global loads
-#endif
-#ifndef RG_NTT_PRIO
-#define RG_NTT_PRIO 0  // A/B knob: 1 = tile loads issued at s_setprio 3 (6% slower), 2 = butterflies at s_setprio 2
-#endif
-#ifndef RG_NTT_SAUX
-#define RG_NTT_SAUX RG_NTT_AUX
-#endif
+// cache policy of the transform's data loads / stores: nt (measured -3% per step against the
+// default, sc1 no better).  The L-round twiddles are staged in LDS per tile for COL and RP tiles
+// (-0.6% per step against per-lane global loads); s_setprio on the tile loads (+6%) or on the
+// butterflies (+5%) measured slower.
+constexpr int kNttAux = 2;
 __device__ __forceinline__ uint64_t rg_bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  const rg_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RG_NTT_AUX);
+  const rg_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kNttAux);
   return pk(v.x, v.y);
 }
 __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   rg_u32x2 v;
   v.x = lo32(x);
   v.y = hi32(x);
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, RG_NTT_SAUX);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, kNttAux);
 }
 
 // PROBE (tuning only; production = 0): 1 = twiddles from registers (no table loads),
@@ -266,15 +259,10 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 // LDS exchanges) of the same launch, timed by bench.py through rg_set_probe
 // LTW: the L round (PAT 2) reads its twiddles from the tile's LDS copy `ltw` (192 entries staged
 // by ntt16_tile: COL tw[64, 256), RP the row's lane-ordered copy) instead of per-lane global loads
-// PIPE (ntt16_pipe): no vector-memory loads at all (an LDS-DMA of the next tile is in flight, and a
-// vector load's vmcnt wait would drain it): the H round's uniform twiddles by scalar loads through
-// the constant address space, the M round's from the workgroup's LDS copy `mtw` (56 entries:
-// mtw[2^k - 8 + j] = tw[2^(G0+k) + (hi << k) + j], k = 3..5), the L round's from `ltw`.
-template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE, bool PIPE = false>
+template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
-                                            uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr,
-                                            const ulonglong2* mtw = nullptr) {
-  constexpr bool LTW = PAT == 2 && (COL || RP) && (RG_NTT_LTW || PIPE);
+                                            uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr) {
+  constexpr bool LTW = PAT == 2 && (COL || RP);
   constexpr int G0 = COL ? 0 : 8;
   // twiddle index independent of the lane: the H round of COL / RP tiles.  (The M round of COL
   // tiles is wave-uniform too, x >> (b + 1) depending on t >> 2 = tid >> 6 only, but scalar loads
@@ -311,20 +299,10 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
       if constexpr ((PROBE & 1) != 0) {
         w[j] = a.w1n + (xof(rho0) >> (b + 1)) + hi;
         wp[j] = a.w1n_p;
-      } else if constexpr (UNIFORM && PIPE) {
-        const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
-        const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
-        typedef const __attribute__((address_space(4))) uint64_t* cptr;
-        w[j] = ((cptr)a.tw)[2 * iu];
-        wp[j] = ((cptr)a.tw)[2 * iu + 1];
       } else if constexpr (UNIFORM) {
         const uint32_t idx = (1u << (G0 + k)) + (hi << k) + (xof(rho0) >> (b + 1));
         const uint32_t iu = __builtin_amdgcn_readfirstlane(idx);
         const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.tw)[iu];
-        w[j] = v.x;
-        wp[j] = v.y;
-      } else if constexpr (PIPE && PAT == 1) {
-        const ulonglong2 v = mtw[(1u << k) - 8u + (xof(rho0) >> (b + 1))];
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (LTW && COL) {
@@ -375,39 +353,8 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
 //        L<->H pad (x>>5).
 // Every pattern pair was checked conflict-free for ds_*_b64 half-wave groups
 // (SQ_LDS_BANK_CONFLICT = 0 for COL in profiles/r01_ntt16_pmc_summary.txt).
-// Which exchanges cross waves (RG_NTT_WL = 1, the default): a wave holds lanes tid in [64w, 64w+64).
-//   ROW: s = tid >> 5, so a wave owns sub-transforms 2w, 2w + 1 whole, and every ROW address
-//        stays in its rows' [288 s, 288 s + 288): every ROW exchange is wave-private.
-//   COL: t >> 2 = w.  M and L put x bits [5, 8) = t >> 2 = w, i.e. the image block
-//        [576 w, 576 w + 576), so M <-> L is wave-private too; only H <-> M crosses waves.
-// A wave-private exchange needs no workgroup barrier: a wave's LDS operations execute in issue
-// order, so wave_lds_fence() (a compiler-level fence) orders its write-then-read and
-// read-then-overwrite.  The tile keeps workgroup barriers only for H <-> M in COL and for the
-// staged L-round twiddles `ltw`, which every wave reads (ROW, COL inverse: one barrier right
-// after the staging, whose global load is issued before the tile's data loads).
-#ifndef RG_NTT_WL
-#define RG_NTT_WL 0  // A/B knob, bit 0: ROW passes wave-local, bit 1: COL passes (0 = round-4 barriers)
-#endif
-#ifndef RG_NTT_STAGGER
-#define RG_NTT_STAGGER 0  // A/B knob: s_sleep argument per quarter of phase offset
-#endif
-#ifndef RG_NTT_YPRIO
-#define RG_NTT_YPRIO 0  // A/B knob: s_setprio for waves 4-7 of the workgroup
-#endif
-__device__ __forceinline__ void ntt_wave_fence() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
-// raw workgroup barrier: waits for the wave's LDS operations only (never vmcnt, so an LDS-DMA in
-// flight survives it); the asm's memory clobber keeps LDS accesses on their side of it
-__device__ __forceinline__ void ntt_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// PIPE: the tile is already in `lds` (ntt16_pipe's LDS-DMA, in the layout each pass's first LDS
-// exchange uses: COL the transposed image, ROW rows [s][x] at pitch 288); each lane reads its first
-// round's points from there instead of HBM, and the barriers are ntt_lds_barrier
-template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0, bool PIPE = false>
-__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw,
-                                           const ulonglong2* mtw = nullptr) {
+template <bool INV, bool COL, bool SCALE, bool CANON, bool RP, int PROBE = 0>
+__device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, uint64_t* lds, ulonglong2* ltw) {
   const uint32_t tid = threadIdx.x;
   const uint32_t s = COL ? (tid & 15u) : (tid >> 5);
   const uint32_t t = COL ? (tid >> 4) : (tid & 31u);
@@ -423,52 +370,14 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const __amdgpu_buffer_rsrc_t twr = rg_buf(a.tw);
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
-  constexpr bool WL = (RG_NTT_WL & (COL ? 2 : 1)) != 0;
-  constexpr bool LTW = (COL || RP) && (RG_NTT_LTW || PIPE) && (PROBE & 1) == 0;
-  auto bar = [&]() {
-    if constexpr (PIPE) ntt_lds_barrier();
-    else __syncthreads();
-  };
-  // an exchange inside one wave's LDS block / one that crosses waves
-  auto wsync = [&]() {
-    if constexpr (WL) ntt_wave_fence();
-    else bar();
-  };
-  if constexpr (RG_NTT_STAGGER != 0) {  // first-generation workgroups of a CU start out of phase
-    if (tile < 1024u) {
-      const uint32_t k = (tile >> 8) & 3u;
-      for (uint32_t i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(RG_NTT_STAGGER);
-    }
+  constexpr bool LTW = (COL || RP) && (PROBE & 1) == 0;
+  if constexpr (LTW) {  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads)
+    const uint32_t base = COL ? 64u : 65536u + hi * 192u;
+    if (tid < 384u)
+      reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
   }
-  if constexpr (RG_NTT_YPRIO != 0) {  // static priority for the workgroup's younger half (waves 4-7)
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256u) __builtin_amdgcn_s_setprio(RG_NTT_YPRIO);
-  }
-  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads); WL: loaded before the
-  // tile's data (its wait then covers this load only) and written to LDS after they are issued
-  uint64_t ltw_word = 0;
-  const uint32_t ltw_base = COL ? 64u : 65536u + hi * 192u;
-  if constexpr (LTW && !WL && !PIPE) {
-    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
-  }
-  if constexpr (LTW && WL && !PIPE) {
-    if (tid < 384u) ltw_word = reinterpret_cast<const uint64_t*>(a.tw + 2ull * ltw_base)[tid];
-  }
-  (void)ltw_base;
-  (void)ltw_word;
-  // ---- global load (RG_NTT_PRIO: the wave issues its tile loads at raised priority)
-  if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(3);
-  if constexpr (PIPE) {
-    if constexpr (COL && !INV) {  // H: the image position 16 x + s + 16 (x >> 3) of x = t + 32 y
-#pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[16 * t + s + 16 * (t >> 3) + 576 * y];
-    } else if constexpr (COL) {  // L: x = 8 t + r
-#pragma unroll
-      for (int r = 0; r < 8; ++r) e[r] = lds[144 * t + s + 16 * r];
-    } else {  // rows [s][x], H: x = t + 32 y
-#pragma unroll
-      for (int y = 0; y < 8; ++y) e[y] = lds[288 * s + t + 32 * y];
-    }
-  } else if constexpr ((PROBE & 4) != 0) {
+  // ---- global load
+  if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = (uint64_t)(tid * 0x9E3779B9u + tile * 8u + (uint32_t)y);
   } else if constexpr (COL) {
@@ -486,13 +395,6 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
   }
-  if constexpr (RG_NTT_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-  if constexpr (RG_NTT_PRIO == 2) __builtin_amdgcn_s_setprio(2);  // 2: butterflies at raised priority
-  if constexpr (LTW && WL && !PIPE) {
-    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = ltw_word;
-    // COL forward reads ltw only after its H -> M barrier
-    if constexpr (!COL || INV) __syncthreads();
-  }
   // PROBE & 4: the result stays live through a store that never fires (values are < 2q < 2^64 - 1)
   auto st64 = [&](uint64_t x, uint32_t voff, uint32_t soff) {
     if constexpr ((PROBE & 4) != 0) {
@@ -506,23 +408,22 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t rH = 288 * s + t, rM = 288 * s + 36 * (t >> 2) + (t & 3), rL9 = 288 * s + 9 * t,
                  rL8 = 288 * s + 8 * t + (t >> 2);
   if constexpr (!INV) {
-    ntt16_round<3, 5, 0, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t);
-    // exchange H -> M (COL: across waves)
+    ntt16_round<3, 5, 0, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    // exchange H -> M
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bH + 576 * y : rH + 36 * y] = e[y];
-    if constexpr (COL) bar();
-    else wsync();
+    __syncthreads();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y];
-    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, nullptr, mtw);
-    wsync();
+    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    __syncthreads();
     // exchange M -> L
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)] = e[y];
-    wsync();
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[COL ? bL + 16 * r : rL9 + r];
-    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, ltw);
+    ntt16_round<2, 0, 2, false, false, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     if (CANON) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = canon_x(e[r], a.q);
@@ -532,10 +433,10 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
       for (int r = 0; r < 8; ++r) st64(e[r], vo, (uint32_t)r << 11);
     } else {  // L -> H through LDS (pad x >> 5), then coalesced rows
-      wsync();
+      __syncthreads();
 #pragma unroll
       for (int r = 0; r < 8; ++r) lds[rL8 + r] = e[r];
-      wsync();
+      __syncthreads();
       const uint32_t vo = ((s << RSH) + t) * 8u;
 #pragma unroll
       for (int y = 0; y < 8; ++y) st64(lds[rH + 33 * y], vo + 256u * y, 0);
@@ -544,29 +445,28 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
 #pragma unroll
       for (int y = 0; y < 8; ++y) lds[rH + 33 * y] = e[y];
-      wsync();
+      __syncthreads();
 #pragma unroll
       for (int r = 0; r < 8; ++r) e[r] = lds[rL8 + r];
-      wsync();
+      __syncthreads();
     }
-    if constexpr (COL && LTW && !WL && !PIPE) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
-    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, ltw);
+    if constexpr (COL && LTW) __syncthreads();  // the staged twiddles (ROW's transpose has its barrier)
+    ntt16_round<2, 0, 2, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     // exchange L -> M
 #pragma unroll
     for (int r = 0; r < 8; ++r) lds[COL ? bL + 16 * r : rL9 + r] = e[r];
-    wsync();
+    __syncthreads();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)];
-    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t, nullptr, mtw);
-    wsync();
-    // exchange M -> H (COL: across waves)
+    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
+    __syncthreads();
+    // exchange M -> H
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bM + offM(y) : rM + 4 * y] = e[y];
-    if constexpr (COL) bar();
-    else wsync();
+    __syncthreads();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bH + 576 * y : rH + 36 * y];
-    ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE, PIPE>(a, twr, e, hi, t);
+    ntt16_round<3, 5, 0, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
     if (CANON) {
 #pragma unroll
       for (int y = 0; y < 8; ++y) e[y] = canon_x(e[y], a.q);
@@ -583,85 +483,11 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   }
 }
 
-#ifndef RG_NTT_LDS_PAD
-#define RG_NTT_LDS_PAD 0  // A/B knob: extra LDS words per workgroup (occupancy experiments)
-#endif
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP = false, int MINW = 1, int PROBE = 0>
 __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
-  __shared__ uint64_t lds[16 * 288 + RG_NTT_LDS_PAD];
-  __shared__ ulonglong2 ltw[(COL || RP) && RG_NTT_LTW ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
+  __shared__ uint64_t lds[16 * 288];
+  __shared__ ulonglong2 ltw[COL || RP ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
   ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds, ltw);
-}
-
-// ----------------------------------------------------------------------------------------
-// Pipelined pass: persistent workgroups (2 per CU, 4 waves/SIMD), each walking tiles at the grid's
-// stride with two LDS images.  While tile k is transformed in image k & 1, tile k + 1 streams
-// from HBM into the other image by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no vmcnt wait
-// until the next tile), so the load latency that the one-tile-per-workgroup pass hides only with
-// 8 resident waves is hidden by the prefetch instead.  The DMA writes each pass's first exchange
-// layout directly: COL the transposed image (8-row blocks of 1 KiB at 1152-B pitch), ROW rows of
-// 2 KiB at the 288-word pitch.  The twiddles a workgroup needs are staged once: its tiles share
-// them (COL: every tile; ROW with RP and a grid that is a multiple of 256: tile & 255, the row, is
-// the same for every tile of a workgroup).  Results equal ntt16_pass's (same rounds, same images).
-__device__ __forceinline__ void ntt_glds16(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
-}
-constexpr int kPipeImg = 16 * 288;  // u64 words per image (36 KiB)
-template <bool INV, bool COL, bool SCALE, bool CANON>
-__global__ __launch_bounds__(512, 1) void ntt16_pipe(Ntt64Args a, uint32_t ntiles) {
-  __shared__ uint64_t img[2 * kPipeImg];
-  __shared__ ulonglong2 ltw[192];
-  __shared__ ulonglong2 mtw[56];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t tile = blockIdx.x;
-  {  // the workgroup's twiddles (ntt16_round's PIPE sources)
-    const uint32_t hi = COL ? 0u : (tile & 255u);
-    const uint64_t* tw = reinterpret_cast<const uint64_t*>(a.tw);
-    if (tid < 384u) reinterpret_cast<uint64_t*>(ltw)[tid] = tw[2ull * (COL ? 64u : 65536u + hi * 192u) + tid];
-    if (tid < 112u) {
-      const uint32_t j = tid >> 1;  // mtw[2^k - 8 + i] = tw[2^(G0+k) + (hi << k) + i], k = 3..5
-      const uint32_t k = j < 8u ? 3u : j < 24u ? 4u : 5u;
-      const uint32_t src = (1u << ((COL ? 0u : 8u) + k)) + (hi << k) + (j + 8u - (1u << k));
-      reinterpret_cast<uint64_t*>(mtw)[tid] = tw[2ull * src + (tid & 1u)];
-    }
-  }
-  const uint32_t img_lds = (uint32_t)(uintptr_t)img;
-  // tile -> LDS-DMA: 32 chunks of 1 KiB (64 lanes x 16 B), 4 per wave
-  auto dma = [&](uint32_t tl, uint32_t buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t c = w + 8u * (uint32_t)i;
-      size_t src;
-      uint32_t dst;  // bytes
-      if constexpr (COL) {  // rows 8c .. 8c + 7 of 16 columns: lane -> row 8c + lane / 8, 2 columns
-        src = ((size_t)(tl >> 4) << 16) + ((tl & 15u) << 4) + (size_t)(8u * c + (lane >> 3)) * 256u + 2u * (lane & 7u);
-        dst = c * 1152u;
-      } else {  // half h of row (tl & 255) of polynomial 16 (tl >> 8) + s
-        const uint32_t sr = c >> 1, h = c & 1u;
-        src = ((size_t)(16u * (tl >> 8) + sr) << 16) + ((tl & 255u) << 8) + 128u * h + 2u * lane;
-        dst = (288u * sr + 128u * h) * 8u;
-      }
-      ntt_glds16(a.in + src, img_lds + buf * (uint32_t)(kPipeImg * 8) + dst);
-    }
-  };
-  if (tile < ntiles) dma(tile, 0);
-  for (uint32_t k = 0; tile < ntiles; ++k, tile += gridDim.x) {
-    // tile k landed (every wave's DMA, then the barrier); the other image is free (tile k - 1 done)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const uint32_t nt = tile + gridDim.x;
-    if (nt < ntiles) dma(nt, (k + 1u) & 1u);
-    ntt16_tile<INV, COL, SCALE, CANON, !COL, 0, true>(a, tile, img + (k & 1u) * kPipeImg, ltw, mtw);
-  }
 }
 
 #endif  // __HIPCC__

@@ -29,16 +29,6 @@ static rg_status launch64(const Ntt64Args& a, size_t polys, hipStream_t st) {
       hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, false, 1, 4>), dim3((unsigned)tiles), dim3(512), 0, st, a);
     return check_launch("ntt16_pass (probe)");
   }
-#ifndef RG_NTT_PIPE
-#define RG_NTT_PIPE 0  // A/B knob: 1 = the pipelined persistent pass (ntt16_pipe) where it applies
-#endif
-  if (RG_NTT_PIPE && polys % 16 == 0 && tiles <= 0xffffffffLL) {
-    // two workgroups per CU; ROW needs a grid that is a multiple of 256 (a workgroup keeps its row)
-    const long long grid = COL ? std::min<long long>(tiles, 512) : (tiles >= 512 ? 512 : 256);
-    hipLaunchKernelGGL((ntt16_pipe<INV, COL, SCALE, CANON>), dim3((unsigned)grid), dim3(512), 0, st, a,
-                       (uint32_t)tiles);
-    return check_launch("ntt16_pipe");
-  }
   if (!COL && polys % 16 == 0)
     hipLaunchKernelGGL((ntt16_pass<INV, COL, SCALE, CANON, true>), dim3((unsigned)tiles), dim3(512), 0, st, a);
   else
