@@ -6,6 +6,8 @@
 
 #include <mutex>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/ringo.h"
@@ -100,6 +102,35 @@ struct DevBuf {
 };
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N), so a body indexes its
+// register arrays with constants (a rolled loop the unroller leaves alone indexes them dynamically)
+template <class F, int... I>
+__host__ __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__host__ __device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Division of a 32-bit index by a launch-constant divisor through the double unit: q = floor(n / d)
+// as trunc((n + 1/2) / d); (n + 1/2) / d keeps 1 / (2 d) from both neighbouring integers, far more
+// than the few-ulp error of one fma on n < 2^32.  3 VALU against ~100 for a 64-bit integer division.
+struct IdxDiv {
+  uint32_t d;
+  double inv, half_inv;  // 1 / d and (1 / d) / 2
+};
+inline IdxDiv make_idxdiv(uint32_t d) {
+  IdxDiv f;
+  f.d = d;
+  f.inv = 1.0 / (double)d;
+  f.half_inv = 0.5 * f.inv;
+  return f;
+}
+__host__ __device__ __forceinline__ uint32_t idx_div(uint32_t n, const IdxDiv& f) {
+  return (uint32_t)fma((double)n, f.inv, f.half_inv);
+}
 
 }  // namespace rg
 

@@ -153,6 +153,7 @@ struct DigitArgs {
   const uint64_t* mask;      // [B][rows][slots][L]
   uint32_t* digits;          // [B][cols+1][rows][d]
   long long total;           // B * (cols+1) * rows * slots
+  IdxDiv d_slots, d_rows, d_cols1;  // total < 2^32: the index split by idx_div (else 64-bit division)
 };
 
 // (num = r * 2^32 + chunk) / b with the precomputed reciprocal, r < b < 2^32
@@ -226,12 +227,23 @@ __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
   const JShape& S = a.s;
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= a.total) return;
-  const int slot = (int)(gid % S.slots);
-  long long r = gid / S.slots;
-  const int row = (int)(r % S.rows);
-  r /= S.rows;
-  const int col = (int)(r % (S.cols + 1));
-  const long long b = r / (S.cols + 1);
+  int slot, row, col;
+  long long b;
+  if (a.total <= 0xffffffffLL) {  // (slot, row, col, b) without 64-bit divisions
+    const uint32_t g = (uint32_t)gid, q1 = idx_div(g, a.d_slots), q2 = idx_div(q1, a.d_rows),
+                   q3 = idx_div(q2, a.d_cols1);
+    slot = (int)(g - q1 * a.d_slots.d);
+    row = (int)(q1 - q2 * a.d_rows.d);
+    col = (int)(q2 - q3 * a.d_cols1.d);
+    b = q3;
+  } else {
+    slot = (int)(gid % S.slots);
+    long long r = gid / S.slots;
+    row = (int)(r % S.rows);
+    r /= S.rows;
+    col = (int)(r % (S.cols + 1));
+    b = r / (S.cols + 1);
+  }
   const long long cs = (long long)S.cols * S.slots;
   const uint64_t* vb = a.v + b * S.nv * L;
   uint32_t* out = a.digits + (((b * (S.cols + 1) + col) * S.rows + row) * (long long)S.d);
@@ -1354,6 +1366,7 @@ constexpr int kCosGroup = 8;
 
 struct SampleArgs {
   JShape s;
+  IdxDiv d_half, d_nm, d_cols;  // mlwe_noise_kernel's index split (pairs < 2^32)
   AesKey key[kNumDom];
   const uint32_t* te0;
   unsigned long long first_commit;
@@ -1981,12 +1994,28 @@ __global__ __launch_bounds__(512) void mlwe_noise_kernel(SampleArgs a) {
   // grid-stride: a bounded grid fills the 64 KiB LDS tables once per workgroup, not once per 512 pairs
   for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < n;
        gid += (long long)gridDim.x * blockDim.x) {
-    const int m = (int)(gid % half);
-    const long long r = gid / half;
-    const int j = (int)(r % nm);
-    const long long r2 = r / nm;
-    const int col = ROUND ? S.cols : (int)(r2 % S.cols);
-    const long long b = ROUND ? r2 : r2 / S.cols;
+    int m, j, col;
+    long long b;
+    if (n <= 0xffffffffLL) {
+      const uint32_t g = (uint32_t)gid, r = idx_div(g, a.d_half), r2 = idx_div(r, a.d_nm);
+      m = (int)(g - r * (uint32_t)half);
+      j = (int)(r - r2 * (uint32_t)nm);
+      if constexpr (ROUND) {
+        col = S.cols;
+        b = r2;
+      } else {
+        const uint32_t r3 = idx_div(r2, a.d_cols);
+        col = (int)(r2 - r3 * (uint32_t)S.cols);
+        b = r3;
+      }
+    } else {
+      m = (int)(gid % half);
+      const long long r = gid / half;
+      j = (int)(r % nm);
+      const long long r2 = r / nm;
+      col = ROUND ? S.cols : (int)(r2 % S.cols);
+      b = ROUND ? r2 : r2 / S.cols;
+    }
     const long long poly = (b * (S.cols + 1) + col) * nm + j;  // (b, col, j)
     long long* out = a.mlwe_noise + poly * S.d;
     const unsigned long long gpoly = a.first_commit * (unsigned long long)(S.cols + 1) * nm + (unsigned long long)poly;
@@ -2030,6 +2059,7 @@ struct UniArgs {
   uint64_t* last_row;  // [B][cols*slots][L]
   uint64_t* mask;      // [B][rows][slots][L]
   long long total;     // B * (cols*slots + rows*slots)
+  IdxDiv d_per;        // cols*slots + rows*slots, for total < 2^32
 };
 
 template <int L>
@@ -2044,7 +2074,14 @@ __global__ __launch_bounds__(512) void uniform_elems_kernel(UniArgs<L> a) {
        gid += (long long)gridDim.x * blockDim.x) [&] {
   const JShape& S = a.s;
   const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
-  const long long b = gid / per, i = gid % per;
+  long long b, i;
+  if (a.total <= 0xffffffffLL) {
+    b = idx_div((uint32_t)gid, a.d_per);
+    i = gid - b * per;
+  } else {
+    b = gid / per;
+    i = gid % per;
+  }
   uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
   if (i == nl - 1) {
 #pragma unroll
@@ -2118,7 +2155,14 @@ __global__ __launch_bounds__(512) void uniform_whole_kernel(UniArgs<L> a, int* f
   const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
   for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
        gid += (long long)gridDim.x * blockDim.x) {
-    const long long b = gid / per, i = gid % per;
+    long long b, i;
+    if (a.total <= 0xffffffffLL) {
+      b = idx_div((uint32_t)gid, a.d_per);
+      i = gid - b * per;
+    } else {
+      b = gid / per;
+      i = gid % per;
+    }
     uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
     if (i == nl - 1) {
 #pragma unroll
@@ -2162,7 +2206,14 @@ __global__ __launch_bounds__(512) void uniform_fix_kernel(UniArgs<L> a, const in
   const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
   for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
        gid += (long long)gridDim.x * blockDim.x) {
-    const long long b = gid / per, i = gid % per;
+    long long b, i;
+    if (a.total <= 0xffffffffLL) {
+      b = idx_div((uint32_t)gid, a.d_per);
+      i = gid - b * per;
+    } else {
+      b = gid / per;
+      i = gid % per;
+    }
     uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
     bool ones = i != nl - 1;
 #pragma unroll
@@ -2688,6 +2739,9 @@ static rg_status launch_digits(const rg_jindo* J, size_t batch, const uint64_t* 
   a.mask = mask;
   a.digits = digits;
   a.total = (long long)batch * (J->p.cols + 1) * J->p.rows * J->p.slots;
+  a.d_slots = make_idxdiv((uint32_t)J->p.slots);
+  a.d_rows = make_idxdiv((uint32_t)J->p.rows);
+  a.d_cols1 = make_idxdiv((uint32_t)(J->p.cols + 1));
   const long long blocks = (a.total + 255) / 256;
   hipLaunchKernelGGL(digits_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   return check_launch("jindo digits");
@@ -3017,6 +3071,7 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.last_row = last;
   a.mask = mask;
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
+  a.d_per = make_idxdiv((uint32_t)(J->p.cols * J->p.slots + J->p.rows * J->p.slots));
   const dim3 ug((unsigned)std::min<long long>((a.total + 511) / 512, 1024));
   if constexpr (L % 2 == 0) {
     if (a.kbytes == 8 * L) {  // whole words: the common draws, then the (practically never) long ones
@@ -3100,6 +3155,9 @@ static rg_status sample_stage(rg_jindo* J, size_t batch, const uint64_t* d_v, si
   const int nm = p.in_msis + p.mlwe;
   a.n_enc_pairs = (long long)batch * (p.cols + 1) * p.rows * (p.d / 2);
   a.n_ml_pairs = (long long)batch * (p.cols + 1) * nm * (p.d / 2);
+  a.d_half = make_idxdiv((uint32_t)(p.d / 2));
+  a.d_nm = make_idxdiv((uint32_t)nm);
+  a.d_cols = make_idxdiv((uint32_t)std::max(p.cols, 1));
   a.batch = (long long)batch;
   {
     const long long npoly = (long long)batch * (p.cols + 1) * p.rows;

@@ -26,9 +26,7 @@
 #pragma once
 #include <stdint.h>
 
-#include <type_traits>
-#include <utility>
-
+#include "common.hpp"
 #include "ntt64.hpp"
 
 namespace rg {
@@ -49,17 +47,8 @@ struct WideArgs {
 
 #if defined(__HIPCC__)
 
-// Compile-time loops: the products are hundreds of partial products, past what the loop unroller
-// fully unrolls, and a rolled loop indexes the digit arrays dynamically (s_set_gpr_idx).
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
+// (static_for, common.hpp: the products are hundreds of partial products, past what the loop
+// unroller fully unrolls, and a rolled loop indexes the digit arrays dynamically)
 // z = x y 2^(-64 L) mod q, canonical, for canonical x, y and q < 2^(64 L - 1): Montgomery on
 // 28-bit digits (K = 64 L / 28: 16 for L = 7, 32 for L = 14; R = 2^(28 K) = 2^(64 L), so the
 // reference's Montgomery tables serve unchanged).  A 28-bit digit product is < 2^56,
