@@ -148,7 +148,10 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
       res = mod_sub(res, shoup_mul((uint64_t)(-(hi + 1)) + 1, 1, P.one_sh, q), q);
     }
     res = mod_add(res, a.corr[lk * 16 + j], q);
-    ring[((lane & 15) * 16 + j) * LK + w] = res;  // [col][j][lk]
+    // [col][j][lk], each 16-word row rotated by 2 col: the wave's 64 lanes (16 columns, rows 16
+    // words apart) then spread over 8 bank pairs instead of one (4-way, not 32-way, conflicts);
+    // even rotations keep each lk pair 16-B aligned for the reads below
+    ring[((lane & 15) * 16 + j) * LK + ((w + 2 * (lane & 15)) & (LK - 1))] = res;
   }
   __syncthreads();
   // 256 rows (col, j) of LK lk (LK * 8 B): LK / 2 threads x 16 B per row
@@ -156,7 +159,8 @@ __global__ __launch_bounds__(64 * LK, 16 / LK) void mac_mfma_kernel(MfmaMacArgs 
     const int row = i / NP, part = i % NP, cl = row >> 4, j = row & 15;
     const long long col = c0 + cl;
     if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r0 = ring[row * LK + 2 * part], r1 = ring[row * LK + 2 * part + 1];
+    const int rp = (2 * part + 2 * cl) & (LK - 1);  // the write's rotation
+    uint64_t r0 = ring[row * LK + rp], r1 = ring[row * LK + rp + 1];
     const long long l = lk0 + 2 * part;
     if (a.C) {
       const ulonglong2 cv = *reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + l);
