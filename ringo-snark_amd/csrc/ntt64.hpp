@@ -237,8 +237,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_buf(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
 // cache policy of the transform's data loads / stores: nt (measured -3% per step against the
-// default, sc1 no better).  The L-round twiddles are staged in LDS per tile for COL and RP tiles
-// (-0.6% per step against per-lane global loads); s_setprio on the tile loads (+6%) or on the
+// default, sc1 no better).  The M- and L-round twiddles are staged in LDS per tile for COL and RP
+// tiles (L round -0.6% per step, M round a further -2.3%, against per-lane global loads that
+// queue behind the tile's HBM traffic); s_setprio on the tile loads (+6%) or on the
 // butterflies (+5%) measured slower.
 constexpr int kNttAux = 2;
 __device__ __forceinline__ uint64_t rg_bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -257,8 +258,9 @@ __device__ __forceinline__ void rg_bstore(uint64_t x, __amdgpu_buffer_rsrc_t r, 
 // 4 = no global data loads / stores (the tile is synthesised from the thread index and its
 // result kept live by a store that never fires): the compute floor (butterflies, twiddle loads,
 // LDS exchanges) of the same launch, timed by bench.py through rg_set_probe
-// LTW: the L round (PAT 2) reads its twiddles from the tile's LDS copy `ltw` (192 entries staged
-// by ntt16_tile: COL tw[64, 256), RP the row's lane-ordered copy) instead of per-lane global loads
+// LTW / MTW: the L round (PAT 2) and the M round (PAT 1) read their twiddles from the tile's LDS
+// copy `ltw` (248 entries staged by ntt16_tile: COL tw[8, 256); RP the row's lane-ordered L-round
+// copy, then its 56 stage 3-5 entries) instead of per-lane global loads
 template <int RK, int LO, int PAT, bool INV, bool SCALE, bool COL, bool RP, int PROBE>
 __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_rsrc_t twr, uint64_t (&e)[8],
                                             uint32_t hi, uint32_t t, const ulonglong2* ltw = nullptr) {
@@ -268,6 +270,7 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
   // tiles is wave-uniform too, x >> (b + 1) depending on t >> 2 = tid >> 6 only, but scalar loads
   // there measured no faster: their lgkmcnt waits also wait for the exchange's LDS traffic.)
   constexpr bool UNIFORM = (COL || RP) && PAT == 0;
+  constexpr bool MTW = PAT == 1 && (COL || RP) && (PROBE & 1) == 0;
   auto xof = [&](int rho) -> uint32_t {
     if (PAT == 0) return t + 32u * rho;
     if (PAT == 1) return ((t >> 2) << 5) | ((uint32_t)rho << 2) | (t & 3u);
@@ -306,11 +309,16 @@ __device__ __forceinline__ void ntt16_round(const Ntt64Args& a, __amdgpu_buffer_
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (LTW && COL) {
-        const ulonglong2 v = ltw[(1u << k) + (xof(rho0) >> (b + 1)) - 64u];
+        const ulonglong2 v = ltw[(1u << k) + (xof(rho0) >> (b + 1)) - 8u];
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (LTW) {
         const ulonglong2 v = ltw[(k == 6 ? 32u * grp : 64u + 32u * (rho0 >> 1)) + t];
+        w[j] = v.x;
+        wp[j] = v.y;
+      } else if constexpr (MTW) {  // M round: COL tw[8, 64) ahead of the L round's; RP the row's stage 3-5 entries after them
+        const ulonglong2 v = COL ? ltw[(1u << k) + (xof(rho0) >> (b + 1)) - 8u]
+                                 : ltw[192u + (k == 3 ? 0u : k == 4 ? 8u : 24u) + (xof(rho0) >> (b + 1))];
         w[j] = v.x;
         wp[j] = v.y;
       } else if constexpr (!COL && PAT == 2) {
@@ -371,10 +379,18 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
   constexpr bool LTW = (COL || RP) && (PROBE & 1) == 0;
-  if constexpr (LTW) {  // the L round's 192 twiddle pairs, one 8-B word per thread (384 threads)
-    const uint32_t base = COL ? 64u : 65536u + hi * 192u;
-    if (tid < 384u)
+  if constexpr (LTW) {  // the M and L rounds' 248 twiddle pairs, one 8-B word per thread (496 threads)
+    const uint32_t base = COL ? 8u : 65536u + hi * 192u;
+    if (tid < (COL ? 496u : 384u))
       reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
+    if constexpr (!COL) {  // the M round's 56 entries (stages 3, 4, 5 of this row)
+      if (tid >= 384u && tid < 496u) {
+        const uint32_t wd = tid - 384u, ent = wd >> 1;
+        const uint32_t kk = ent < 8u ? 3u : ent < 24u ? 4u : 5u, j = ent - (kk == 3u ? 0u : kk == 4u ? 8u : 24u);
+        const uint32_t idx = (1u << (8u + kk)) + (hi << kk) + j;
+        reinterpret_cast<uint64_t*>(ltw)[2u * (192u + ent) + (wd & 1u)] = reinterpret_cast<const uint64_t*>(a.tw)[2u * idx + (wd & 1u)];
+      }
+    }
   }
   // ---- global load
   if constexpr ((PROBE & 4) != 0) {
@@ -415,7 +431,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     __syncthreads();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y];
-    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 2, 1, false, false, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     __syncthreads();
     // exchange M -> L
 #pragma unroll
@@ -458,7 +474,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
     __syncthreads();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[COL ? bM + offM(y) : rM + 4 * y + (y >> 1)];
-    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t);
+    ntt16_round<3, 2, 1, true, SCALE, COL, RP, PROBE>(a, twr, e, hi, t, ltw);
     __syncthreads();
     // exchange M -> H
 #pragma unroll
@@ -486,7 +502,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 template <bool INV, bool COL, bool SCALE, bool CANON, bool RP = false, int MINW = 1, int PROBE = 0>
 __global__ __launch_bounds__(512, MINW) void ntt16_pass(Ntt64Args a) {
   __shared__ uint64_t lds[16 * 288];
-  __shared__ ulonglong2 ltw[COL || RP ? 192 : 1];  // 39 KiB per workgroup with lds: 4 per CU
+  __shared__ ulonglong2 ltw[COL || RP ? 248 : 1];  // 39.9 KiB per workgroup with lds: 4 per CU
   ntt16_tile<INV, COL, SCALE, CANON, RP, PROBE>(a, blockIdx.x, lds, ltw);
 }
 
