@@ -206,15 +206,35 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
   __syncthreads();
   // ---- the P stages
   const int nbf = cpt * (NP >> 1);
+  // twiddle index of butterfly bf at local stage g
+  auto tw_idx = [&](int g, int bf) -> long long {
+    const int c = bf >> (P - 1), p = bf & ((NP >> 1) - 1), bitpos = P - 1 - g;
+    const int x0 = ((p >> bitpos) << (bitpos + 1)) | (p & ((1 << bitpos) - 1));
+    const long long r = (s0 + c) & ((1LL << subs_log) - 1);
+    const long long hi = (r >> logS) & ((1LL << a.G0) - 1);
+    return (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
+  };
+  // L = 14: the next butterfly's twiddle is loaded one butterfly ahead (across the stage barrier),
+  // so its L2 latency hides behind the current product, which 2 waves/SIMD do not (zp880 +1.3%);
+  // L = 7 (4 waves/SIMD) loads it in place (the prefetch's extra VGPRs and index work cost 1%)
+  constexpr bool PF = L >= 14;
+  uint32_t wn[D];
+  auto fetch = [&](long long idx) {
+    const uint64_t* tp = a.tw + idx * L;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const uint64_t t = tp[l];
+      wn[2 * l] = lo32(t);
+      wn[2 * l + 1] = hi32(t);
+    }
+  };
+  if (PF && (int)threadIdx.x < nbf) fetch(tw_idx(INV ? P - 1 : 0, (int)threadIdx.x));
   for (int st = 0; st < P; ++st) {
     const int g = INV ? P - 1 - st : st;  // local stage (global G0 + g)
     const int bitpos = P - 1 - g;
     for (int bf = threadIdx.x; bf < nbf; bf += kWideThreads) {
       const int c = bf >> (P - 1), p = bf & ((NP >> 1) - 1);
       const int x0 = ((p >> bitpos) << (bitpos + 1)) | (p & ((1 << bitpos) - 1)), x1 = x0 | (1 << bitpos);
-      const long long s = s0 + c;
-      const long long r = s & ((1LL << subs_log) - 1);
-      const long long hi = (r >> logS) & ((1LL << a.G0) - 1);
       uint32_t u[D], v[D], w[D];
 #pragma unroll
       for (int l = 0; l < L; ++l) {
@@ -224,32 +244,38 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         v[2 * l] = lo32(vv);
         v[2 * l + 1] = hi32(vv);
       }
-      auto load_w = [&]() {
-        const long long idx = (1LL << (a.G0 + g)) + (hi << g) + (x0 >> (bitpos + 1));
-        const uint64_t* tp = a.tw + idx * L;
+      auto take_w = [&]() {
+        if constexpr (!PF) fetch(tw_idx(g, bf));
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-          const uint64_t t = tp[l];
-          w[2 * l] = lo32(t);
-          w[2 * l + 1] = hi32(t);
+        for (int i = 0; i < D; ++i) w[i] = wn[i];
+        if constexpr (PF) {  // the next butterfly of this stage, else this thread's first of the next stage
+          int nb = bf + kWideThreads, ns = st;
+          if (nb >= nbf) {
+            nb = (int)threadIdx.x;
+            ++ns;
+          }
+          if (ns < P) fetch(tw_idx(INV ? P - 1 - ns : ns, nb));
         }
       };
       uint32_t nu[D], nv[D];
       if constexpr (!INV) {  // ntt.go:254-259
-        load_w();
+        take_w();
         uint32_t t[D];
         mont(t, v, w);
         add_wide<D>(nu, u, t, q);
         sub_wide<D>(nv, u, t, q);
       } else {  // ntt.go:365-370 with each stage's outputs halved: log N stages give N^-1 (242-243)
         uint32_t d[D], s[D];
+        if constexpr (PF) take_w();  // the next twiddle's loads issue ahead of this butterfly's work
         add_wide<D>(s, u, v, q);
         half_wide<D>(nu, s, q);
         sub_wide<D>(d, u, v, q);
-        // u and v are dead here: the twiddle load is held behind the add / sub so the 14-limb
-        // kernel's live set at the product is d, w and nu, as the forward's is u, v and w
-        __builtin_amdgcn_sched_barrier(0);
-        load_w();
+        // u and v are dead here: without the prefetch the twiddle load is held behind the add /
+        // sub so the live set at the product is d, w and nu, as the forward's is u, v and w
+        if constexpr (!PF) {
+          __builtin_amdgcn_sched_barrier(0);
+          take_w();
+        }
         mont(nv, d, w);  // w = twInv / 2
       }
 #pragma unroll
@@ -258,7 +284,10 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         lds[l * plane + c * NP + x1] = pk(nv[2 * l], nv[2 * l + 1]);
       }
     }
-    __syncthreads();
+    // LDS-only barrier: __syncthreads() would also wait for the twiddle prefetch (vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
   // ---- LDS -> HBM
   for (int f = threadIdx.x; f < W; f += kWideThreads) {
