@@ -379,19 +379,27 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
   const uint32_t hi = COL ? 0u : RP ? (uint32_t)__builtin_amdgcn_readfirstlane(tile & 255u) : (((tile << 4) + s) & 255u);
   uint64_t e[8];
   constexpr bool LTW = (COL || RP) && (PROBE & 1) == 0;
-  if constexpr (LTW) {  // the M and L rounds' 248 twiddle pairs, one 8-B word per thread (496 threads)
-    const uint32_t base = COL ? 8u : 65536u + hi * 192u;
-    if (tid < (COL ? 496u : 384u))
-      reinterpret_cast<uint64_t*>(ltw)[tid] = reinterpret_cast<const uint64_t*>(a.tw + 2ull * base)[tid];
-    if constexpr (!COL) {  // the M round's 56 entries (stages 3, 4, 5 of this row)
-      if (tid >= 384u && tid < 496u) {
-        const uint32_t wd = tid - 384u, ent = wd >> 1;
-        const uint32_t kk = ent < 8u ? 3u : ent < 24u ? 4u : 5u, j = ent - (kk == 3u ? 0u : kk == 4u ? 8u : 24u);
-        const uint32_t idx = (1u << (8u + kk)) + (hi << kk) + j;
-        reinterpret_cast<uint64_t*>(ltw)[2u * (192u + ent) + (wd & 1u)] = reinterpret_cast<const uint64_t*>(a.tw)[2u * idx + (wd & 1u)];
-      }
-    }
+  // The M and L rounds' 248 twiddle pairs, one 8-B word per thread (496 threads): the word is
+  // loaded after the tile's data loads and written to LDS just before the first barrier, so no
+  // wave waits for it before issuing its data loads (the first load's latency would otherwise
+  // open every tile).  COL: tw[8, 256); RP: the row's lane-ordered L-round copy, then its 56
+  // stage 3-5 entries.
+  const bool stv_on = LTW && tid < 496u;
+  uint32_t st_src = 0, st_dst = tid;
+  if constexpr (COL) {
+    st_src = 16u + tid;
+  } else if (tid < 384u) {
+    st_src = 2u * (65536u + hi * 192u) + tid;
+  } else {
+    const uint32_t wd = tid - 384u, ent = wd >> 1;
+    const uint32_t kk = ent < 8u ? 3u : ent < 24u ? 4u : 5u, j = ent - (kk == 3u ? 0u : kk == 4u ? 8u : 24u);
+    st_src = 2u * ((1u << (8u + kk)) + (hi << kk) + j) + (wd & 1u);
+    st_dst = 2u * (192u + ent) + (wd & 1u);
   }
+  uint64_t stv = 0;
+  auto stage_write = [&]() {
+    if (stv_on) reinterpret_cast<uint64_t*>(ltw)[st_dst] = stv;
+  };
   // ---- global load
   if constexpr ((PROBE & 4) != 0) {
 #pragma unroll
@@ -411,6 +419,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = rg_bload(rin, vo + 256u * y, 0);
   }
+  if (stv_on) stv = reinterpret_cast<const uint64_t*>(a.tw)[st_src];
   // PROBE & 4: the result stays live through a store that never fires (values are < 2q < 2^64 - 1)
   auto st64 = [&](uint64_t x, uint32_t voff, uint32_t soff) {
     if constexpr ((PROBE & 4) != 0) {
@@ -425,6 +434,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
                  rL8 = 288 * s + 8 * t + (t >> 2);
   if constexpr (!INV) {
     ntt16_round<3, 5, 0, false, false, COL, RP, PROBE>(a, twr, e, hi, t);
+    stage_write();
     // exchange H -> M
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[COL ? bH + 576 * y : rH + 36 * y] = e[y];
@@ -458,6 +468,7 @@ __device__ __forceinline__ void ntt16_tile(const Ntt64Args& a, uint32_t tile, ui
       for (int y = 0; y < 8; ++y) st64(lds[rH + 33 * y], vo + 256u * y, 0);
     }
   } else {
+    stage_write();
     if constexpr (!COL) {  // ROW inverse: loaded in H, transpose to L (pad x >> 5)
 #pragma unroll
       for (int y = 0; y < 8; ++y) lds[rH + 33 * y] = e[y];
