@@ -478,43 +478,67 @@ __device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
   return c < 0 ? mod_neg(m, P.q) : m;
 }
 
-template <int MINW>
+template <int MINW, bool PAIR1>
 __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs a) {
   __shared__ uint64_t lds_all[kPrepWaves][2 * 288];
   extern __shared__ ulonglong2 tw_lds[];  // the nq limbs' forward tables (w, w'), [nq][256]: dynamic LDS
   const JShape& S = a.s;
   const int nq = S.nq;
-  // slot 0 of each limb's table (unused by the transform) holds (2^64 w1, Shoup) for stage 0
-  for (int i = threadIdx.x; i < nq * 256; i += blockDim.x)
-    tw_lds[i] = (i & 255) ? a.R.fwd[i] : make_ulonglong2(a.R.p[i >> 8].rw1, a.R.p[i >> 8].rw1_sh);
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
   const int wv = threadIdx.x >> 6;
   uint64_t* lds = lds_all[wv];
   const long long job = (long long)blockIdx.x * kPrepWaves + wv;
-  if (job >= a.n_enc + a.n_ml) return;
+  const bool has = job < a.n_enc + a.n_ml;
   const bool is_enc = job < a.n_enc;
-  uint64_t* dst;
+  uint64_t* dst = nullptr;
   const uint32_t* dg = nullptr;
-  const long long* nz;
-  if (is_enc) {
+  const long long* nz = nullptr;
+  bool skip = false;
+  if (has && is_enc) {
     const long long pj = job;
     const int cr = (int)(pj % ((long long)(S.cols + 1) * S.rows));
     dst = a.enc + pj * nq * 256;
-    if (enc_skipped(S, cr / S.rows, cr % S.rows)) {  // Opening.Encode[i][j] stays zero
-      for (int k = (int)lane; k < nq * 256; k += 64) dst[k] = 0;
-      return;
-    }
+    skip = enc_skipped(S, cr / S.rows, cr % S.rows);  // Opening.Encode[i][j] stays zero
     dg = a.digits + pj * 256;
     nz = a.enc_noise + pj * 256;
-  } else {
+  } else if (has) {
     const long long mj = job - a.n_enc;
     dst = a.mlwe + mj * nq * 256;
     nz = a.mlwe_noise + mj * 256;
   }
+  // the job's inputs (noise, shifted noise, digits).  PAIR1 (nq <= 2, every configs ring): loaded
+  // ahead of the table staging so the two loads' latencies overlap (configs[2] +1.4%); otherwise
+  // read per limb pair after it, rather than held across the NTT
+  long long cv[8], csv[8];
+  uint32_t dv[8];
+  auto load_in = [&]() {
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+      const int k = (int)t + 32 * y;
+      cv[y] = nz[k];
+      if (is_enc) {
+        const int ks = k - S.slots;
+        csv[y] = ks >= 0 ? nz[ks] : nz[ks + 256];
+        dv[y] = dg[k];
+      } else {
+        csv[y] = 0;
+        dv[y] = 0;
+      }
+    }
+  };
+  if (PAIR1 && has && !skip) load_in();
+  // slot 0 of each limb's table (unused by the transform) holds (2^64 w1, Shoup) for stage 0
+  for (int i = threadIdx.x; i < nq * 256; i += blockDim.x)
+    tw_lds[i] = (i & 255) ? a.R.fwd[i] : make_ulonglong2(a.R.p[i >> 8].rw1, a.R.p[i >> 8].rw1_sh);
+  __syncthreads();
+  if (!has) return;
+  if (skip) {
+    for (int k = (int)lane; k < nq * 256; k += 64) dst[k] = 0;
+    return;
+  }
   const uint32_t rH = 288 * hs + t, rM = 288 * hs + 36 * (t >> 2) + (t & 3), rL9 = 288 * hs + 9 * t,
                  rL8 = 288 * hs + 8 * t + (t >> 2);
-  for (int l0 = 0; l0 < nq; l0 += 2) {
+  auto pair = [&](const int l0) {
     const int limb = l0 + (int)hs;
     const bool active = limb < nq;
     const int lc = active ? limb : l0;
@@ -525,22 +549,20 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
     // signed integer v = dg +- s' - s b when that fits (|s| <= 2^61 / b, |s'| < 2^61); the MLWE
     // finalize is MForm(setCoeffSigned(s)) (prover.go:130-141): v = s.  MForm is a factor 2^64 on
     // every coefficient, so it rides on NTT stage 0: e holds v mod q (one add when |v| < q), and
-    // stage 0 multiplies by 2^64 and 2^64 w1 instead of w1.  Inputs are (re)read per limb pair
-    // rather than held across the NTT.
+    // stage 0 multiplies by 2^64 and 2^64 w1 instead of w1.
     uint64_t e[8];
     uint32_t big = 0;  // bit y: coefficient t + 32 y takes the term-by-term reduction
 #pragma unroll
     for (int y = 0; y < 8; ++y) {
       const int k = (int)t + 32 * y;
-      const long long c = nz[k];
+      const long long c = cv[y];
       long long v = c;
       bool ok = true;
       if (is_enc) {
-        const int ks = k - S.slots;
-        const long long cs = ks >= 0 ? nz[ks] : nz[ks + 256];
+        const long long cs = csv[y];
         const uint64_t s2 = k < S.slots ? 0ull - (uint64_t)cs : (uint64_t)cs;  // wrapped coefficients negate
         ok = c >= -a.clim && c <= a.clim && cs > -(1LL << 61) && cs < (1LL << 61);
-        v = (long long)((uint64_t)dg[k] + s2 - (uint64_t)c * S.base);
+        v = (long long)((uint64_t)dv[y] + s2 - (uint64_t)c * S.base);
       }
       const uint64_t r = v < 0 ? (uint64_t)v + q : (uint64_t)v;  // v mod q when -q <= v < q
       ok = ok && r < q;
@@ -599,6 +621,14 @@ __global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs
       for (int y = 0; y < 8; ++y) o[t + 32 * y] = lds[rH + 33 * y];
     }
     wave_lds_fence();
+  };
+  if constexpr (PAIR1) {
+    pair(0);
+  } else {
+    for (int l0 = 0; l0 < nq; l0 += 2) {
+      load_in();
+      pair(l0);
+    }
   }
 }
 
@@ -2991,11 +3021,13 @@ static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_
     const dim3 g((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
     const size_t twl = (size_t)nq * 256 * sizeof(ulonglong2);
     if (pw >= 8)
-      hipLaunchKernelGGL(prep256_kernel<8>, g, b, twl, st, pa);
+      hipLaunchKernelGGL((prep256_kernel<8, false>), g, b, twl, st, pa);
+    else if (pw >= 6 && nq <= 2)
+      hipLaunchKernelGGL((prep256_kernel<6, true>), g, b, twl, st, pa);
     else if (pw >= 6)
-      hipLaunchKernelGGL(prep256_kernel<6>, g, b, twl, st, pa);
+      hipLaunchKernelGGL((prep256_kernel<6, false>), g, b, twl, st, pa);
     else
-      hipLaunchKernelGGL(prep256_kernel<1>, g, b, twl, st, pa);
+      hipLaunchKernelGGL((prep256_kernel<1, false>), g, b, twl, st, pa);
   } else {
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   }
