@@ -65,17 +65,21 @@ rg_status ntt64_run(const NttLaunch& p, hipStream_t st, bool* handled) {
       a.in = p.in + b0 * N;
       a.out = p.out + b0 * N;
       a.G0 = 0;
+      a.rev = 0;
       RG_TRY((launch64<false, true, false, false>(a, nb, st)));
       a.in = a.out;
       a.G0 = 8;
+      a.rev = 1;  // reverse tile order: reads what the first pass wrote last first (ntt64.hpp)
       RG_TRY((launch64<false, false, false, true>(a, nb, st)));
     } else {
       a.in = p.in + b0 * N;
       a.out = p.out + b0 * N;
       a.G0 = 8;
+      a.rev = 0;
       RG_TRY((launch64<true, false, false, false>(a, nb, st)));
       a.in = a.out;
       a.G0 = 0;
+      a.rev = 1;  // reverse tile order: reads what the first pass wrote last first (ntt64.hpp)
       RG_TRY((launch64<true, true, true, true>(a, nb, st)));
     }
   }
