@@ -478,16 +478,16 @@ __device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
   return c < 0 ? mod_neg(m, P.q) : m;
 }
 
-template <int MINW, bool PAIR1>
-__global__ __launch_bounds__(64 * kPrepWaves, MINW) void prep256_kernel(PrepArgs a) {
-  __shared__ uint64_t lds_all[kPrepWaves][2 * 288];
+template <int MINW, bool PAIR1, int WAVES = kPrepWaves>
+__global__ __launch_bounds__(64 * WAVES, MINW) void prep256_kernel(PrepArgs a) {
+  __shared__ uint64_t lds_all[WAVES][2 * 288];
   extern __shared__ ulonglong2 tw_lds[];  // the nq limbs' forward tables (w, w'), [nq][256]: dynamic LDS
   const JShape& S = a.s;
   const int nq = S.nq;
   const uint32_t lane = threadIdx.x & 63u, t = lane & 31u, hs = lane >> 5;
   const int wv = threadIdx.x >> 6;
   uint64_t* lds = lds_all[wv];
-  const long long job = (long long)blockIdx.x * kPrepWaves + wv;
+  const long long job = (long long)blockIdx.x * WAVES + wv;
   const bool has = job < a.n_enc + a.n_ml;
   const bool is_enc = job < a.n_enc;
   uint64_t* dst = nullptr;
@@ -3018,9 +3018,17 @@ static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_
       const char* e = knob(Knob::JindoPrepW);
       return e ? atoi(e) : 6;
     }();
-    const dim3 g((unsigned)((pa.n_enc + n_ml + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
+    const long long jobs = pa.n_enc + n_ml;
+    const dim3 g((unsigned)((jobs + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
     const size_t twl = (size_t)nq * 256 * sizeof(ulonglong2);
-    if (pw >= 8)
+    // large launches (configs[4]'s encode prep, 2.4 M jobs): 12-wave workgroups, so each table
+    // staging serves 12 polynomials instead of 4 (configs[4] +1.2%; at configs[2]'s 0.3 M jobs the
+    // 4-wave form is 1% faster: profiles/r05ao_prep_workgroup_ab.txt)
+    constexpr int kBigWaves = 12;
+    if (pw >= 6 && pw < 8 && nq <= 2 && jobs >= (1LL << 20)) {
+      hipLaunchKernelGGL((prep256_kernel<2, true, kBigWaves>), dim3((unsigned)((jobs + kBigWaves - 1) / kBigWaves)),
+                         dim3(64 * kBigWaves), twl, st, pa);
+    } else if (pw >= 8)
       hipLaunchKernelGGL((prep256_kernel<8, false>), g, b, twl, st, pa);
     else if (pw >= 6 && nq <= 2)
       hipLaunchKernelGGL((prep256_kernel<6, true>), g, b, twl, st, pa);
