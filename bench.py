@@ -287,9 +287,27 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world,
             dist.barrier()
         return time.perf_counter() - t0, ev.total_ms()
 
+    def selfcheck(sampled):
+        """Commit c = batch - 1 of the batch just timed, re-run alone (a 1-commit call at its own
+        first_commit: the small-batch dispatch, 4-wave prep256, no 12-wave workgroups) must equal
+        the batch's output for it, bit for bit.  Cheap, outside the timed region."""
+        c = batch - 1
+        sh1 = params.shapes(1)
+        o1 = {k: torch.empty(sh1[k], dtype=torch.int64, device=dev) for k in outs}
+        if sampled:
+            prv.commit_sampled_dev(1, v[c:], nv, seeds, first + c, o1["incom"], o1["enc"], o1["mlwe_out"], o1["com"],
+                                   stream)
+        else:
+            prv.commit_dev(1, v[c:], nv, last[c:], mask[c:], en[c:], mn[c:], o1["incom"], o1["enc"], o1["mlwe_out"],
+                           o1["com"], stream)
+        torch.cuda.synchronize()
+        return all(torch.equal(o1[k][0], outs[k][c]) for k in outs)
+
     line = "j14" if cfg_name == "t14_b1" else "j16"
     wall_i, kern_i = timed(step_injected, line + "_injected")
+    ok_i = selfcheck(False)
     wall, kern = timed(step_sampled, line)
+    ok_s = selfcheck(True)
     nm = params.in_msis + params.mlwe
     opening_words = (params.dcmp * params.nqo * params.d + (params.cols + 1) * params.rows * params.nq * params.d +
                      (params.cols + 1) * nm * params.nq * params.d)
@@ -300,7 +318,8 @@ def jindo_bench(torch, ringo, dist, cfg_name, batch, steps, warmup, rank, world,
     inj_words = (nv * L + params.cols * params.slots * L + params.rows * params.slots * L +
                  (params.cols + 1) * params.rows * params.d + (params.cols + 1) * nm * params.d)
     res = dict(wall_s=wall, kernel_ms=kern, commits=batch * steps, bytes_per_commit=bytes_per_commit,
-               injected_wall_s=wall_i, injected_kernel_ms=kern_i, injected_bytes_per_commit=8 * (inj_words + out_words))
+               injected_wall_s=wall_i, injected_kernel_ms=kern_i, injected_bytes_per_commit=8 * (inj_words + out_words),
+               selfcheck=ok_s, selfcheck_injected=ok_i)
     if eval_steps and P["batch"] > 1:
         res["eval"] = eval_bench(torch, prv, dist, P, params, batch, outs, eval_steps, g, dev, opening_words)
     return res
@@ -776,8 +795,9 @@ def main():
             continue
         js = max(2, args.steps // 2)
         jr = jindo_bench(torch, ringo, dist, cfg, jb, js, 1, rank, world, eval_steps=js)
-        jms, jk, jmi, jki = reduce_max(torch, dist, jr["wall_s"] * 1000.0 / js, jr["kernel_ms"],
-                                       jr["injected_wall_s"] * 1000.0 / js, jr["injected_kernel_ms"])
+        jms, jk, jmi, jki, jbad = reduce_max(torch, dist, jr["wall_s"] * 1000.0 / js, jr["kernel_ms"],
+                                             jr["injected_wall_s"] * 1000.0 / js, jr["injected_kernel_ms"],
+                                             0.0 if jr["selfcheck"] and jr["selfcheck_injected"] else 1.0)
         trj, vbj = line_counters(C, key, jb, jk / js)
         name = "jindo_commit" if cfg == "t14_b1" else "jindo_commit_2e16"
         out[name] = {"value": world * jb / (jms / 1000.0), "unit": "commits/s",
@@ -787,6 +807,10 @@ def main():
                      "batch_per_gpu": jb, "ms_per_batch": jms, "n_gpus": world,
                      "achieved_GBs": jr["bytes_per_commit"] * jr["commits"] / (jk / 1000.0) / 1e9,
                      "bytes_per_commit": jr["bytes_per_commit"], "traffic_per_commit": trj, "valu": vbj,
+                     "selfcheck_single_commit_rerun": jbad == 0.0,
+                     "selfcheck_note": "on every rank, commit batch-1 of the timed batch re-run alone (1-commit "
+                                       "call at its first_commit: the small-batch kernels) equals the batch's output "
+                                       "bit for bit, for both the sampled and the injected path",
                      "randomness": "sampled on the device inside the timed step (AES-256-CTR UniformSampler "
                                    "instances, TwinCDT / COSAC / rounded Gaussian, MustSetRandom): Prover.Commit end "
                                    "to end (rg_jindo_commit_sampled_dev)",

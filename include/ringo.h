@@ -47,7 +47,13 @@ typedef enum {
 const char* rg_status_string(int status);
 /* Thread-local text of the last device error (hipGetErrorString + call site). */
 const char* rg_last_error(void);
-/* Library build id (kernel set + gfx target), for logs. */
+/* Library build id (kernel set + gfx target + sampler layout), for logs.  The string ends in
+ * "sampler-layout N" with N = RG_SAMPLER_LAYOUT of the build: the partition of the device
+ * samplers' draws into UniformSampler instances (rg_jindo_seeds).  The same seeds and
+ * first_commit give the same sampled commitments only between builds of one layout.
+ *   1: rounds 3-4 (COSAC instances per group of 16 coefficients)
+ *   2: round 5 on (COSAC instances per group of 8 coefficients) */
+#define RG_SAMPLER_LAYOUT 2
 const char* rg_version(void);
 
 /* ------------------------------------------------------------------------------------ */

@@ -29,7 +29,11 @@ const char* rg_status_string(int s) {
 
 const char* rg_last_error(void) { return g_last_error.c_str(); }
 
-const char* rg_version(void) { return "libringo 0.1 gfx950 (ntt, vec, jindo)"; }
+#define RG_STR2(x) #x
+#define RG_STR(x) RG_STR2(x)
+const char* rg_version(void) {
+  return "libringo 0.2 gfx950 (ntt, vec, jindo) sampler-layout " RG_STR(RG_SAMPLER_LAYOUT);
+}
 
 rg_status rg_field_create(int limbs, const uint64_t* q_le, rg_field** out) {
   if (!out || !q_le) return RG_ERR_INVALID;

@@ -4105,16 +4105,24 @@ rg_status rg_jindo_commit_sampled_dev(const rg_jindo* J, size_t batch, const uin
     ax = &x;
   }
   hipStream_t s_cos = ax ? ax->s[0] : st, s_ml = ax ? ax->s[1] : st;
-  RG_TRY(sample_stage(Jm, batch, d_v, nv, seeds, first_commit, sc->last.as<uint64_t>(), sc->mask.as<uint64_t>(), en, mn,
-                      digits, sc, st, s_cos, s_ml, ax ? ax->e[0] : nullptr, ax ? ax->e[1] : nullptr));
-  RG_TRY(prep_launch(Jm, batch, nv, digits, en, mn, d_enc, d_mlwe, kPrepMlwe, s_ml));
+  rg_status s = sample_stage(Jm, batch, d_v, nv, seeds, first_commit, sc->last.as<uint64_t>(), sc->mask.as<uint64_t>(),
+                             en, mn, digits, sc, st, s_cos, s_ml, ax ? ax->e[0] : nullptr, ax ? ax->e[1] : nullptr);
+  if (s == RG_OK) s = prep_launch(Jm, batch, nv, digits, en, mn, d_enc, d_mlwe, kPrepMlwe, s_ml);
   // (the TwinCDT rows' prep right behind cdt2, beside cosac2, measured no faster: r05i)
-  if (ax) {  // join: the encode prep needs both samplers' noise; the core needs the MLWE prep
-    RG_HIP(hipEventRecord(ax->e[2], s_cos));
-    RG_HIP(hipEventRecord(ax->e[3], s_ml));
-    RG_HIP(hipStreamWaitEvent(st, ax->e[2], 0));
-    RG_HIP(hipStreamWaitEvent(st, ax->e[3], 0));
+  if (ax) {
+    // join: the encode prep needs both samplers' noise; the core needs the MLWE prep.  Joined on
+    // every exit path, so that after a failed launch the caller's stream still orders whatever
+    // helper work was queued before this handle's scratch (wq, en, mn) is reused; the first error
+    // is the one returned
+    const hipError_t j[4] = {hipEventRecord(ax->e[2], s_cos), hipEventRecord(ax->e[3], s_ml),
+                             hipStreamWaitEvent(st, ax->e[2], 0), hipStreamWaitEvent(st, ax->e[3], 0)};
+    for (hipError_t e : j)
+      if (e != hipSuccess && s == RG_OK) {
+        set_last_error(std::string("jindo sampled commit: joining the helper streams: ") + hipGetErrorString(e));
+        s = RG_ERR_DEVICE;
+      }
   }
+  RG_TRY(s);
   RG_TRY(prep_launch(Jm, batch, nv, digits, en, mn, d_enc, d_mlwe, kPrepEnc, st));
   return commit_core(Jm, batch, d_enc, d_mlwe, d_incom, d_com, sc, st);
 }

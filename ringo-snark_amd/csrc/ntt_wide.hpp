@@ -284,10 +284,13 @@ __global__ __launch_bounds__(kWideThreads, 2) void ntt_wide_pass(WideArgs a) {  
         lds[l * plane + c * NP + x1] = pk(nv[2 * l], nv[2 * l + 1]);
       }
     }
-    // LDS-only barrier: __syncthreads() would also wait for the twiddle prefetch (vmcnt(0))
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // LDS-only barrier: __syncthreads() would also wait for the twiddle prefetch (vmcnt(0)).  The
+    // workgroup fences restricted to the local address space order the LDS stage exchange (they
+    // compile to lgkmcnt(0) + s_barrier) and leave the global prefetch in flight; only LDS is
+    // shared between stages, global memory is written once after the last one
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   }
   // ---- LDS -> HBM
   for (int f = threadIdx.x; f < W; f += kWideThreads) {

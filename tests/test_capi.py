@@ -20,6 +20,16 @@ def test_library_exports_every_header_symbol():
     assert set(_lib._SIGS) <= set(names)
 
 
+def test_version_names_sampler_layout():
+    """rg_version ends in the build's sampler layout (include/ringo.h RG_SAMPLER_LAYOUT): round 5
+    renumbered the COSAC instances (groups of 8), so sampled commitments differ from layout 1's."""
+    import re
+    m = re.search(r"#define RG_SAMPLER_LAYOUT (\d+)", open(_lib.HEADER).read())
+    assert m and int(m.group(1)) == 2
+    v = _lib.lib().rg_version().decode()
+    assert v.startswith("libringo 0.2 gfx950") and v.endswith("sampler-layout " + m.group(1)), v
+
+
 def test_status_strings_match_reference_panics():
     L = _lib.lib()
     assert L.rg_status_string(-1) == b"inconsistent input(s)"

@@ -198,11 +198,11 @@ def test_sample_moments_2e16():
 
 
 def test_commit_sampled_two_stream_split():
-    """A sampled batch of >= 64 commits runs as two halves on two streams (the caller's and the
-    handle's auxiliary one, joined by events): equal, bit for bit, to the single-stream runs of
-    the same commits (rg_jindo_sample_dev + rg_jindo_commit_dev of the whole batch, and two
-    sub-batches of < 64 with their first_commit offsets), on a caller stream that is not the null
-    stream."""
+    """A sampled batch runs as one DAG over the caller's stream and two helper streams of it
+    (samplers and the MLWE prep beside the TwinCDT / encode chain, joined by events): equal, bit
+    for bit, to other schedules of the same commits (rg_jindo_sample_dev + rg_jindo_commit_dev of
+    the whole batch on one stream, and two sub-batches with their first_commit offsets), on a
+    caller stream that is not the null stream."""
     import torch
     name = "t10_b1"
     P = PARAMS[name]
