@@ -275,8 +275,9 @@ size_t rg_jindo_scratch_bytes(const rg_jindo* j, size_t batch);
 rg_status rg_jindo_release_stream(rg_jindo* j, void* stream);
 /* Which kernel runs the inner (prover.go:149-157) and outer (:180-191) Ajtai products of this
  * handle: RG_MAC_MFMA (mac_mfma.hip, the matrix cores; needs canonical inputs, see
- * rg_jindo_commit_core_dev), RG_MAC_VALU3 (mac3h), RG_MAC_GENERIC (mac_kernel).  Introspection
- * only; no reference counterpart. */
+ * rg_jindo_commit_core_dev) or RG_MAC_GENERIC (mac_kernel).  RG_MAC_VALU3 is never returned by this
+ * build (the VALU mac3h kernel was removed in round 6; tools/experiments/jindo_knob_kernels.patch).
+ * Introspection only; no reference counterpart. */
 enum { RG_MAC_GENERIC = 0, RG_MAC_VALU3 = 1, RG_MAC_MFMA = 2 };
 rg_status rg_jindo_mac_kinds(const rg_jindo* j, int* inner, int* outer);
 

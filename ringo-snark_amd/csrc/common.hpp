@@ -21,16 +21,10 @@ void set_last_error(const std::string& msg);
 // (tools/experiments/knobs_env.hip), reads them from the RINGO_* environment and honours
 // rg_set_probe; the production library has no environment access at all.
 enum class Knob : int {
-  NttKernel,   // RINGO_NTT_KERNEL   r2 | r8 | r*: generic single-word / q255 pass kernels; stage: wide fields per stage
+  NttKernel,   // RINGO_NTT_KERNEL   r*: generic single-word / q255 pass kernels; stage: wide fields per stage
   NttChunkMb,  // RINGO_NTT_CHUNK_MB polys per pass pair bounded to this many MiB
-  NttPrefetch, // RINGO_NTT_PREFETCH 0: no next-tile register prefetch in ntt_r2
-  NttWgPerCu,  // RINGO_NTT_WG_PER_CU persistent ntt_r8 grid size
-  NttR8Pf,     // RINGO_NTT_R8_PF    1: persistent prefetching ntt_r8
-  JindoPrep,   // RINGO_JINDO_PREP   l: workgroup-per-polynomial prep_kernel
-  JindoPrepW,  // RINGO_JINDO_PREP_W minimum waves/SIMD of prep256 (1, 6, 8)
-  JindoMac,    // RINGO_JINDO_MAC    h: mac3h, l: mac_kernel instead of the MFMA MAC
+  JindoMac,    // RINGO_JINDO_MAC    l: mac_kernel instead of the MFMA MAC
   JindoSplit,  // RINGO_JINDO_SPLIT  0: commit_sampled on the caller's stream only
-  JindoEval,   // RINGO_JINDO_EVAL   mac: Evaluate's batch combination on mac_kernel, not dot_split_kernel
   JindoUniTries,  // RINGO_JINDO_UNI_TRIES n: uniform_whole_kernel gives up after n tries (tests the fix-up path)
   Count
 };

@@ -16,8 +16,9 @@
 //                      sum_k In[j][k]*Enc[k] + sum_k CK.MLWE[j][k]*MLWE[k] + MLWE[mlwe+j]
 //                      (prover.go:149-157): exact sums reduced once (MulCoeffsMontgomeryThenAdd
 //                      summed == (sum a*b) * 2^-64 mod q).  mac_mfma_kernel (mac_mfma.hip, the
-//                      matrix cores) where its digit bound holds; else mac3h_kernel (VALU);
-//                      mac_kernel for primes >= 2^60 or J > 16.
+//                      matrix cores) where its digit bound holds (every configs shape); else
+//                      mac_kernel (exact 128/160-bit sums, any prime and J).  Round 2-5's VALU
+//                      Karatsuba MAC (mac3h) is tools/experiments/jindo_knob_kernels.patch.
 //   4. round_kernel    workgroup per polynomial: IMForm, INTT, centred CRT (Garner, up to 4
 //                      primes), floor shift by the cut, Euclidean mod q', MForm, NTT in the
 //                      destination ring (prover.go:164-176, rns.go:76-114).
@@ -779,315 +780,6 @@ static rg_status launch_mac(const MacArgs& m, hipStream_t st) {
   return RG_OK;
 }
 
-// Column-lane MAC for primes q < 2^60 (every Jindo ring prime of the configs).
-// The product is the per-(limb, coeff) modular GEMM out[col][j] = sum_t A[j][t] B[col][t]
-// (prover.go:144-157, 180-191).  A workgroup owns 64 columns (one per lane) x 8 (limb, coeff)
-// (one per wave):
-//  * the commit key is stored split and transposed, As[lk][t][JP] = a0 | a1 << 32 with
-//    a = a0 + a1 2^29, so a wave's slice of a tile (8 terms x JP) is one contiguous 1-KB run;
-//  * B tiles (8 terms x 8 lk x 64 columns, 64-B rows from HBM) and the key slices are staged
-//    through LDS, double-buffered, the next tile's loads in flight during the current tile's
-//    products; key words are wave-uniform LDS reads (broadcast);
-//  * with b = b0 + b1 2^29, a*b = a0b0 + (a0b1 + a1b0) 2^29 + a1b1 2^58: three 64-bit
-//    accumulators absorb `fold` terms with plain v_mad_u64_u32 (4 VALU per MAC, no carries)
-//    before folding into the exact 128-bit sum, the same integer as Acc's, reduced once;
-//  * results are transposed through LDS so every store (and the + MLWE[mlwe + j] read) is a
-//    64-B row.
-constexpr int kMac3Tc = 8;  // terms per LDS tile
-struct Mac3Args {
-  long long per_col, ncols;
-  int J, T1, T2, fold;  // fold: a multiple of kMac3Tc
-  int Tp;               // T1 + T2 rounded up to kMac3Tc (the key's zero-padded term count)
-  const uint64_t* As;   // [per_col][Tp][JP]
-  const uint32_t* Ss;   // [per_col][Tp][JP]  a0 + a1 of the same key words (the Karatsuba middle)
-  const uint64_t* B1;
-  long long b1_col, b1_term;
-  const uint64_t* B2;
-  long long b2_col, b2_term;
-  const uint64_t* C;  // nullable
-  long long c_col, c_j;
-  uint64_t* out;  // [ncols][J][per_col]
-  int d;
-  RnsPrime P[kMaxQ];
-};
-struct Mac3Acc {
-  uint64_t s00, s01, s11, lo, hi;
-};
-__device__ __forceinline__ void mac3_fold(Mac3Acc& a) {
-  uint32_t c0 = 0, c1 = 0, c2 = 0;
-  a.lo = addc(a.lo, a.s00, c0);
-  a.lo = addc(a.lo, a.s01 << 29, c1);
-  a.lo = addc(a.lo, a.s11 << 58, c2);
-  a.hi += (a.s01 >> 35) + (a.s11 >> 6) + c0 + c1 + c2;
-  a.s00 = a.s01 = a.s11 = 0;
-}
-
-// Karatsuba accumulators: sm = sum (a0 + a1)(b0 + b1), so the middle sum is
-// s01 = sm - s00 - s11 (exact: sm holds every product of the four); folded like Mac3Acc
-__device__ __forceinline__ void mac3k_fold(Mac3Acc& a) {
-  a.s01 -= a.s00 + a.s11;
-  mac3_fold(a);
-}
-
-// ---- LDS-DMA staging (global_load_lds_dwordx4) ------------------------------------------
-// Register-staged tiles (round 1's mac3_kernel: 232 VGPRs, 2 waves/SIMD, one tile in flight)
-// could not cover HBM latency.  Tiles go HBM -> LDS directly (no VGPR cost), in a ring of
-// kMacRing buffers: while tile i is multiplied, tiles i+1 and i+2 are in flight.  A tile's loads
-// are retired by a counted `s_waitcnt vmcnt` (only the loads issued after it may stay
-// outstanding) and a raw s_barrier (a __syncthreads would drain every DMA).  The removed
-// register-staged and one-column forms are tools/experiments/mac3_mac3g.patch.
-constexpr int kMacRing = 3;
-
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// ---- mac3h: two columns per lane, half the outputs per wave ----------------------------------
-// The one-column form (mac3g, removed) was LDS-bound, not VALU-bound: every MAC needs its key words as a wave-uniform LDS read
-// (12 B: a0 | a1 and a0 + a1), and a uniform ds_read_b128 still costs the LDS 4 cycles, so the
-// key reads of 8 waves alone (3,072 LDS cycles per tile) outrun a SIMD's multiplies (~3,456);
-// its B reads (lane stride 64 B) are 8-way bank conflicts on top.  Here a lane owns TWO
-// columns (c, c + 64) and a wave HALF the outputs (JP / 2) of one lk, so each broadcast key word
-// feeds two columns: key LDS cycles per MAC halve at the same 160 accumulator VGPRs.  B goes
-// to LDS as [tt][2-lk chunk m][128 columns][2 lk] (one LDS-DMA = one chunk of 64 columns), so a
-// lane's b64 read has a 16-B lane stride: 2-way, not 8-way.  Workgroup = 128 columns x 4 lk;
-// blocks are mapped XCD-major so the 4 lk groups sharing a 128-B line of B run on one XCD.
-template <int JP, int JG>
-__global__ __launch_bounds__(256 * JG, 1) void mac3h_kernel(Mac3Args a) {
-  constexpr int NLK = 4, JH = JP / JG, NC = 128, NW = 4 * JG;  // JG output groups: NW waves
-  constexpr int BW = kMac3Tc * 2 * NC * 2;  // B image words per buffer: [tt][m][col][2]
-  constexpr int AW = NLK * kMac3Tc * JP;    // A image words: [lk][tt][JP]
-  constexpr int SW = NLK * kMac3Tc * JP / 2;  // S image words (u32 sums): [lk][tt][JP]
-  constexpr int NA = (JP + 3) / 4;          // A wave-instructions per tile (16 JP chunks of 16 B)
-  constexpr int NS = (JP + 7) / 8;          // S wave-instructions per tile (8 JP chunks)
-  constexpr int RW = BW + AW + SW;
-  static_assert(JP * NLK * NC <= kMacRing * RW, "output stage must fit the ring");
-  static_assert(JP % JG == 0 && (JG == 2 || JG == 4), "output groups");
-  constexpr int BPW = 32 / NW;  // B wave-instructions per wave per tile (32 per tile)
-  __shared__ uint64_t ring[kMacRing * RW];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lkw = w & 3, jh = w >> 2;
-  static_assert(NS <= NA, "wait counts");
-  unsigned g = blockIdx.x;
-  if ((gridDim.x & 7) == 0) g = (g & 7) * (gridDim.x >> 3) + (g >> 3);  // XCD-major
-  const long long nlkg = a.per_col / NLK;
-  const long long lk0 = (long long)(g % nlkg) * NLK, c0 = (long long)(g / nlkg) * NC;
-  const int T = a.T1 + a.T2;
-  const int ntile = a.Tp / kMac3Tc;
-  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-  auto issue = [&](int tile, int buf) {
-    const uint32_t bbase = ring_lds + (uint32_t)(buf * RW) * 8u;
-    // B: 32 instructions (tt, m, column half h) per tile, BPW per wave
-#pragma unroll
-    for (int k = 0; k < BPW; ++k) {
-      const int idx = w * BPW + k, tt = idx >> 2, m = (idx >> 1) & 1, h = idx & 1;
-      int t = tile * kMac3Tc + tt;
-      if (t >= T) t = T - 1;  // clamped: the key's padded terms are zero
-      const uint64_t* rowbase = t < a.T1 ? a.B1 + (long long)t * a.b1_term : a.B2 + (long long)(t - a.T1) * a.b2_term;
-      const long long colstride = t < a.T1 ? a.b1_col : a.b2_col;
-      long long col = c0 + h * 64 + lane;
-      if (col >= a.ncols) col = a.ncols - 1;
-      glds16(rowbase + col * colstride + lk0 + 2 * m, bbase + (uint32_t)(((tt * 2 + m) * NC + h * 64) * 2) * 8u);
-    }
-    if (w < NA) {  // A: lane's 16 B = key words (lk, tt, j..j+1)
-      const int c = w * 64 + lane;
-      if (c < 16 * JP) {
-        const int u = 2 * c;
-        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
-        glds16(a.As + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r, bbase + (uint32_t)(BW + w * 128) * 8u);
-      }
-    }
-    if (w < NS) {  // S: lane's 16 B = four u32 sums (lk, tt, j..j+3)
-      const int c = w * 64 + lane;
-      if (c < 8 * JP) {
-        const int u = 4 * c;
-        const int lk = u / (kMac3Tc * JP), r = u % (kMac3Tc * JP);
-        glds16(a.Ss + ((lk0 + lk) * a.Tp + (long long)tile * kMac3Tc) * JP + r,
-               bbase + (uint32_t)(BW + AW) * 8u + (uint32_t)w * 1024u);
-      }
-    }
-  };
-  Mac3Acc acc[2][JH];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < JH; ++j) acc[h][j] = Mac3Acc{0, 0, 0, 0, 0};
-  issue(0, 0);
-  if (ntile > 1) issue(1, 1);
-  int since = 0;
-  for (int it = 0; it < ntile; ++it) {
-    const int buf = it % kMacRing;
-    if (it + 1 < ntile) {  // only tile it+1's loads may stay outstanding
-      if (w < NS) wait_vm<BPW + 2>();
-      else if (w < NA) wait_vm<BPW + 1>();
-      else wait_vm<BPW>();
-    } else {
-      wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (it + 2 < ntile) issue(it + 2, (it + 2) % kMacRing);
-    const uint64_t* L = ring + buf * RW + ((lkw >> 1) * NC + lane) * 2 + (lkw & 1);
-    const uint64_t* LA = ring + buf * RW + BW + lkw * (kMac3Tc * JP) + jh * JH;
-    const uint32_t* LS = reinterpret_cast<const uint32_t*>(ring + buf * RW + BW + AW) + lkw * (kMac3Tc * JP) + jh * JH;
-#pragma unroll
-    for (int tt = 0; tt < kMac3Tc; ++tt) {
-      uint32_t b0[2], b1[2], bs[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint64_t b = L[tt * (2 * NC * 2) + h * 128];
-        b0[h] = (uint32_t)b & 0x1fffffffu;
-        b1[h] = (uint32_t)(b >> 29);
-        bs[h] = b0[h] + b1[h];
-      }
-#pragma unroll
-      for (int j = 0; j < JH; ++j) {
-        const uint64_t av = LA[tt * JP + j];
-        const uint32_t a0 = (uint32_t)av, a1 = (uint32_t)(av >> 32), as = LS[tt * JP + j];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          Mac3Acc& z = acc[h][j];
-          z.s00 = mad64(a0, b0[h], z.s00);
-          z.s01 = mad64(as, bs[h], z.s01);
-          z.s11 = mad64(a1, b1[h], z.s11);
-        }
-      }
-    }
-    since += kMac3Tc;
-    if (since >= a.fold) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < JH; ++j) mac3k_fold(acc[h][j]);
-      since = 0;
-    }
-  }
-  __syncthreads();
-  const int lk = (int)lk0 + lkw;
-  const RnsPrime& P = a.P[lk / a.d];
-  const uint64_t q = P.q;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < JH; ++j) {
-      mac3k_fold(acc[h][j]);
-      uint64_t r = sh_mul(acc[h][j].lo, P.rinv, P.rinv_sh, q);
-      r = mod_add(r, sh_mul(acc[h][j].hi, 1, P.one_sh, q), q);
-      ring[((jh * JH + j) * NLK + lkw) * NC + h * 64 + lane] = r;  // [j][lk][col]
-    }
-  __syncthreads();
-  const uint64_t qa = a.P[(int)(lk0 / a.d)].q;  // 4 lk never straddle a limb (d % 8 == 0)
-  for (int pidx = tid; pidx < JP * NC; pidx += 256 * JG) {
-    const int c = pidx & (NC - 1), j = pidx / NC;
-    const long long col = c0 + c;
-    if (j >= a.J || col >= a.ncols) continue;
-    uint64_t r[NLK];
-#pragma unroll
-    for (int x = 0; x < NLK; ++x) r[x] = ring[(j * NLK + x) * NC + c];
-    if (a.C) {
-      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(a.C + col * a.c_col + (long long)j * a.c_j + lk0);
-#pragma unroll
-      for (int i = 0; i < NLK / 2; ++i) {
-        const ulonglong2 cv = cp[i];
-        r[2 * i] = mod_add(cv.x, r[2 * i], qa);
-        r[2 * i + 1] = mod_add(cv.y, r[2 * i + 1], qa);
-      }
-    }
-    ulonglong2* op = reinterpret_cast<ulonglong2*>(a.out + (col * a.J + j) * a.per_col + lk0);
-#pragma unroll
-    for (int i = 0; i < NLK / 2; ++i) op[i] = make_ulonglong2(r[2 * i], r[2 * i + 1]);
-  }
-}
-
-// J padded to the instantiated widths (J = 9..10 padded to 12: the 1,024-thread mac3h<12,4> measured
-// faster than a 512-thread mac3h<10,2>, whose 110 KiB ring capped it at 2 waves/SIMD)
-static int mac3_jp(int J) {
-  static const int w[] = {4, 6, 8, 12, 12, 16};
-  for (int x : w)
-    if (J <= x) return x;
-  return 0;
-}
-
-// fold period: the largest F <= 32 with F * max partial product < 2^64 in every accumulator
-// (a0 b0 < 2^58, two of a0 b1, a1 b0 < 2^bits per term, a1 b1 < 2^(2 (bits - 29))),
-// rounded down to whole tiles
-static int mac3_fold_period(const RnsPrime* P, int nl) {
-  int bits = 29;
-  for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
-  // the Karatsuba middle: (a0 + a1)(b0 + b1) <= smax^2, smax = 2^29 - 1 + max a1 (exact in q)
-  double smax = 0;
-  for (int l = 0; l < nl; ++l) smax = std::max(smax, (double)((1ull << 29) - 1 + ((P[l].q - 1) >> 29)));
-  int f = 32;
-  while (f > 1 && ((double)f * 2.0 * std::ldexp(1.0, bits) > std::ldexp(1.0, 64) ||
-                   (double)f * std::ldexp(1.0, 2 * std::max(0, bits - 29)) > std::ldexp(1.0, 64) ||
-                   (double)f * smax * smax >= std::ldexp(1.0, 64)))
-    f >>= 1;
-  return f & ~(kMac3Tc - 1);
-}
-
-// eligible: a fold period of at least one tile, J <= 16, the exact sum below 2^128, 8 | d
-static bool mac3_ok(const RnsPrime* P, int nl, int J, int T, int d) {
-  int bits = 0;
-  for (int l = 0; l < nl; ++l) bits = std::max(bits, 64 - __builtin_clzll(P[l].q - 1));
-  const bool fits128 = (double)T * std::ldexp(1.0, 2 * bits) < std::ldexp(1.0, 128);
-  return mac3_fold_period(P, nl) >= kMac3Tc && mac3_jp(J) > 0 && fits128 && d % 8 == 0;
-}
-
-static rg_status launch_mac3(const Mac3Args& m, hipStream_t st) {
-  // mac3h, 4 output groups (1,024 threads) where JP allows, 2 otherwise
-  const dim3 gh((unsigned)((m.ncols + 127) / 128 * (m.per_col / 4)));
-  const dim3 b2(512), b4(1024);
-  switch (mac3_jp(m.J)) {
-    case 4: hipLaunchKernelGGL((mac3h_kernel<4, 2>), gh, b2, 0, st, m); break;
-    case 6: hipLaunchKernelGGL((mac3h_kernel<6, 2>), gh, b2, 0, st, m); break;
-    case 8: hipLaunchKernelGGL((mac3h_kernel<8, 4>), gh, b4, 0, st, m); break;
-    case 10: hipLaunchKernelGGL((mac3h_kernel<10, 2>), gh, b2, 0, st, m); break;
-    case 12: hipLaunchKernelGGL((mac3h_kernel<12, 4>), gh, b4, 0, st, m); break;
-    default: hipLaunchKernelGGL((mac3h_kernel<16, 4>), gh, b4, 0, st, m); break;
-  }
-  return check_launch("jindo mac3h");
-}
-
-// the commit key of one MAC, split and transposed for mac3h_kernel (on the device):
-// out[lk][t][JP] = a0 | a1 << 32 of A_set[j][t][lk] (t over set 1 then set 2; rows j >= J and terms
-// t >= T1 + T2, up to the padded count Tp, zero)
-__global__ __launch_bounds__(256) void mac3_key_kernel(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J,
-                                                       int JP, long long per_col, uint64_t* out) {
-  const int T = T1 + T2, Tp = (T + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= per_col * Tp * JP) return;
-  const int j = (int)(i % JP);
-  const int t = (int)((i / JP) % Tp);
-  const long long lk = i / ((long long)JP * Tp);
-  uint64_t x = 0;
-  if (j < J && t < T) x = t < T1 ? A1[((long long)j * T1 + t) * per_col + lk] : A2[((long long)j * T2 + (t - T1)) * per_col + lk];
-  out[i] = (x & 0x1fffffffull) | ((x >> 29) << 32);
-  reinterpret_cast<uint32_t*>(out + per_col * Tp * JP)[i] = (uint32_t)(x & 0x1fffffffull) + (uint32_t)(x >> 29);
-}
-
-static rg_status mac3_key_dev(const uint64_t* A1, int T1, const uint64_t* A2, int T2, int J, size_t per_col, DevBuf& out,
-                              hipStream_t st) {
-  const int JP = mac3_jp(J);
-  const int Tp = (T1 + T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
-  const long long n = (long long)per_col * Tp * JP;
-  RG_TRY(out.alloc((size_t)n * 12 + 16));  // a0 | a1 << 32 words, then the u32 sums a0 + a1
-  hipLaunchKernelGGL(mac3_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A1, T1, A2, T2, J, JP,
-                     (long long)per_col, out.as<uint64_t>());
-  return check_launch("jindo mac3 key");
-}
 
 // ------------------------------------------------------------------------------------------
 // 4. round: IMForm -> INTT -> centred CRT -> floor shift -> mod q' -> MForm -> NTT
@@ -2510,10 +2202,8 @@ struct rg_jindo {
   rg::CrtDev crt_q, crt_o;
   rg::DstDev dst_o, dst_q;
   rg::DevBuf ck_in, ck_mlwe, ck_out;  // the commit key, device-resident (entities.go:21-73 layouts)
-  rg::DevBuf ck3_in, ck3_out;         // the same, split + transposed for mac3h_kernel (inner, outer; built only where it runs)
-  bool mac3_q = false, mac3_o = false;
   rg::DevBuf ckm_in, ckm_out;  // the same as base-256 digits for mac_mfma (inner, outer)
-  int mfma_q = 0, mfma_o = 0;  // digits per residue of the MFMA MAC (0: mac3h / mac_kernel)
+  int mfma_q = 0, mfma_o = 0;  // digits per residue of the MFMA MAC (0: mac_kernel)
   uint64_t base_inv;
   std::mutex mu;  // guards `scratch` and `aux`
   std::map<hipStream_t, std::unique_ptr<rg_jindo_scratch>> scratch;
@@ -2795,44 +2485,6 @@ static rg_status stream_scratch(rg_jindo* J, size_t batch, hipStream_t st, rg_ji
   return RG_OK;
 }
 
-// RINGO_JINDO_PREP=legacy selects the workgroup-per-polynomial prep kernel (A/B switch)
-static bool prep_legacy() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = knob(Knob::JindoPrep);
-    v = (e && e[0] == 'l') ? 1 : 0;
-  }
-  return v == 1;
-}
-
-// MacArgs (legacy kernel layout) -> Mac3Args
-static Mac3Args mac3_args(const MacArgs& m, const uint64_t* As, int fold) {
-  Mac3Args a;
-  memset(&a, 0, sizeof(a));
-  a.per_col = (long long)m.nl * m.d;
-  a.ncols = m.ncols;
-  a.J = m.J;
-  a.T1 = m.T1;
-  a.T2 = m.T2;
-  a.fold = fold;
-  a.Tp = (m.T1 + m.T2 + kMac3Tc - 1) / kMac3Tc * kMac3Tc;
-  a.As = As;
-  a.Ss = reinterpret_cast<const uint32_t*>(As + a.per_col * a.Tp * mac3_jp(m.J));
-  a.B1 = m.B1;
-  a.b1_col = m.b1_col;
-  a.b1_term = m.b1_term;
-  a.B2 = m.B2;
-  a.b2_col = m.b2_col;
-  a.b2_term = m.b2_term;
-  a.C = m.C;
-  a.c_col = m.c_col;
-  a.c_j = m.c_j;
-  a.out = m.out;
-  a.d = m.d;
-  for (int l = 0; l < m.nl; ++l) a.P[l] = m.P[l];
-  return a;
-}
-
 static MfmaPrime mfma_prime(const RnsPrime& P) { return MfmaPrime{P.q, P.rinv, P.rinv_sh, P.one_sh}; }
 
 // MacArgs (legacy kernel layout) -> MfmaMacArgs over the digit key `key` (mac_mfma_key_dev)
@@ -2923,8 +2575,6 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   for (int l = 0; l < nq; ++l) ma.P[l] = J->rq[l];
   if (J->mfma_q) {
     RG_TRY(launch_mac_mfma(mfma_args(ma, J->ckm_in), J->mfma_q, st));
-  } else if (J->mac3_q) {
-    RG_TRY(launch_mac3(mac3_args(ma, J->ck3_in.as<uint64_t>(), mac3_fold_period(J->rq, nq)), st));
   } else {
     RG_TRY(launch_mac(ma, st));
   }
@@ -2961,8 +2611,6 @@ static rg_status commit_core(rg_jindo* J, size_t batch, const uint64_t* d_enc, c
   for (int l = 0; l < nqo; ++l) mo.P[l] = J->ro[l];
   if (J->mfma_o) {
     RG_TRY(launch_mac_mfma(mfma_args(mo, J->ckm_out), J->mfma_o, st));
-  } else if (J->mac3_o) {
-    RG_TRY(launch_mac3(mac3_args(mo, J->ck3_out.as<uint64_t>(), mac3_fold_period(J->ro, nqo)), st));
   } else {
     RG_TRY(launch_mac(mo, st));
   }
@@ -3013,11 +2661,7 @@ static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_
   if (pa.n_enc + n_ml == 0) return RG_OK;
   bool q61 = true;  // prep256's lazy [0, 8q) needs q < 2^61 (every configs ring prime is <= 59 bits)
   for (int l = 0; l < nq; ++l) q61 = q61 && J->rq[l].q < (1ull << 61);
-  if (d == 256 && q61 && !prep_legacy()) {
-    static const int pw = [] {  // RINGO_JINDO_PREP_W: minimum waves per SIMD for prep256 (tuning)
-      const char* e = knob(Knob::JindoPrepW);
-      return e ? atoi(e) : 6;
-    }();
+  if (d == 256 && q61) {  // else prep_kernel: a workgroup per polynomial, any d and q
     const long long jobs = pa.n_enc + n_ml;
     const dim3 g((unsigned)((jobs + kPrepWaves - 1) / kPrepWaves)), b(64 * kPrepWaves);
     const size_t twl = (size_t)nq * 256 * sizeof(ulonglong2);
@@ -3025,17 +2669,15 @@ static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_
     // staging serves 12 polynomials instead of 4 (configs[4] +1.2%; at configs[2]'s 0.3 M jobs the
     // 4-wave form is 1% faster: profiles/r05ao_prep_workgroup_ab.txt)
     constexpr int kBigWaves = 12;
-    if (pw >= 6 && pw < 8 && nq <= 2 && jobs >= (1LL << 20)) {
+    // (minimum waves per SIMD 8 or 1 instead of 6, round 2-5's RINGO_JINDO_PREP_W: slower at both
+    // configs shapes, removed in round 6)
+    if (nq <= 2 && jobs >= (1LL << 20)) {
       hipLaunchKernelGGL((prep256_kernel<2, true, kBigWaves>), dim3((unsigned)((jobs + kBigWaves - 1) / kBigWaves)),
                          dim3(64 * kBigWaves), twl, st, pa);
-    } else if (pw >= 8)
-      hipLaunchKernelGGL((prep256_kernel<8, false>), g, b, twl, st, pa);
-    else if (pw >= 6 && nq <= 2)
+    } else if (nq <= 2)
       hipLaunchKernelGGL((prep256_kernel<6, true>), g, b, twl, st, pa);
-    else if (pw >= 6)
-      hipLaunchKernelGGL((prep256_kernel<6, false>), g, b, twl, st, pa);
     else
-      hipLaunchKernelGGL((prep256_kernel<1, false>), g, b, twl, st, pa);
+      hipLaunchKernelGGL((prep256_kernel<6, false>), g, b, twl, st, pa);
   } else {
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)(pa.n_enc + n_ml)), dim3(256), 0, st, pa);
   }
@@ -3334,8 +2976,7 @@ static rg_status launch_dot(const MacArgs& m, hipStream_t st) {
   uint64_t qmax = 0;
   for (int l = 0; l < m.nl; ++l) qmax = std::max(qmax, m.P[l].q);
   const bool narrow = 2.0 * log2((double)(qmax - 1)) + log2((double)m.T1 + 1.0) < 127.5;
-  const char* k = knob(Knob::JindoEval);  // experiments build: RINGO_JINDO_EVAL=mac (A/B)
-  if (m.J != 1 || m.T2 != 0 || m.C || !narrow || (m.nl * m.d) % 64 != 0 || (k && k[0] == 'm'))
+  if (m.J != 1 || m.T2 != 0 || m.C || !narrow || (m.nl * m.d) % 64 != 0)
     return launch_mac(m, st);
   const long long blocks = (m.ncols + kDotNC - 1) / kDotNC * ((long long)m.nl * m.d / 64);
   hipLaunchKernelGGL(dot_split_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
@@ -3721,15 +3362,15 @@ static rg_status jindo_new(const rg_jindo_params* p, rg_jindo** out, rg_jindo** 
 }
 
 // The commit key is device-resident from here on: ck_in/ck_mlwe/ck_out hold it in the
-// entities.go layouts; the MAC kernels' key images (MFMA digits, or mac3h's split + transposed
+// entities.go layouts; the MAC kernels' key images (the MFMA MAC's digits
 // words) are built from them on the device, only for the MAC each product runs on.
 static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
   const rg_jindo_params& p = J->p;
-  // RINGO_JINDO_MAC (experiments build): l = mac_kernel, h = mac3h (VALU); default = the MFMA MAC
-  // where it applies, else mac3h where it applies, else mac_kernel
+  // RINGO_JINDO_MAC (experiments build): l = mac_kernel; default = the MFMA MAC where it applies,
+  // else mac_kernel
   const char* mk = knob(Knob::JindoMac);
   const bool legacy = mk && mk[0] == 'l';
-  const bool no_mfma = legacy || (mk && mk[0] == 'h');
+  const bool no_mfma = legacy;
   const size_t pcq = (size_t)p.nq * p.d, pco = (size_t)p.nqo * p.d;
   {
     uint64_t pq[kMaxQ], po[kMaxQ];
@@ -3745,11 +3386,6 @@ static rg_status finish_ck(rg_jindo* J, hipStream_t st) {
       RG_TRY(mac_mfma_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, (long long)pco, p.d,
                               J->mfma_o, mo, p.nqo, J->ckm_out, st));
   }
-  J->mac3_q = !legacy && !J->mfma_q && mac3_ok(J->rq, p.nq, p.in_msis, p.rows + p.mlwe, p.d);
-  J->mac3_o = !legacy && !J->mfma_o && mac3_ok(J->ro, p.nqo, p.out_msis, p.dcmp, p.d);
-  if (J->mac3_q)
-    RG_TRY(mac3_key_dev(J->ck_in.as<uint64_t>(), p.rows, J->ck_mlwe.as<uint64_t>(), p.mlwe, p.in_msis, pcq, J->ck3_in, st));
-  if (J->mac3_o) RG_TRY(mac3_key_dev(J->ck_out.as<uint64_t>(), p.dcmp, nullptr, 0, p.out_msis, pco, J->ck3_out, st));
   RG_HIP(hipStreamSynchronize(st));
   return RG_OK;
 }
@@ -4151,8 +3787,8 @@ rg_status rg_jindo_release_stream(rg_jindo* J, void* stream) {
 
 rg_status rg_jindo_mac_kinds(const rg_jindo* J, int* inner, int* outer) {
   if (!J || !inner || !outer) return RG_ERR_INVALID;
-  *inner = J->mfma_q ? RG_MAC_MFMA : J->mac3_q ? RG_MAC_VALU3 : RG_MAC_GENERIC;
-  *outer = J->mfma_o ? RG_MAC_MFMA : J->mac3_o ? RG_MAC_VALU3 : RG_MAC_GENERIC;
+  *inner = J->mfma_q ? RG_MAC_MFMA : RG_MAC_GENERIC;
+  *outer = J->mfma_o ? RG_MAC_MFMA : RG_MAC_GENERIC;
   return RG_OK;
 }
 

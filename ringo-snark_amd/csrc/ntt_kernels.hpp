@@ -809,25 +809,12 @@ static rg_status launch_r2_pf(const NttArgs<L>& a, hipStream_t st) {
   return check_launch("ntt_r2");
 }
 
-// RINGO_NTT_PREFETCH=0 disables the next-tile register prefetch (A/B switch for tuning)
-static inline bool r2_prefetch_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = knob(Knob::NttPrefetch);
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
+// the next-tile register prefetch at L = 1 (q >= 2^63: the CIOS single-word fields; Shoup fields
+// take ntt_r8); none at L >= 2, where the tile's registers leave no room for it
 template <int L, bool INV, bool SHOUP, bool SCALE, bool COL>
 static rg_status launch_r2(const NttArgs<L>& a, hipStream_t st) {
-  const bool pf = L == 1 && r2_prefetch_enabled();
-  if (L == 1 && SHOUP && a.qlo1) {
-    if (pf) return launch_r2_pf<L, INV, SHOUP, SCALE, COL, true, true>(a, st);
-    return launch_r2_pf<L, INV, SHOUP, SCALE, COL, false, true>(a, st);
-  }
-  if (pf) return launch_r2_pf<L, INV, SHOUP, SCALE, COL, true, false>(a, st);
-  return launch_r2_pf<L, INV, SHOUP, SCALE, COL, false, false>(a, st);
+  static_assert(!(L == 1 && SHOUP), "single-word Shoup fields run on ntt_r8 (run_tiled)");
+  return launch_r2_pf<L, INV, SHOUP, SCALE, COL, L == 1, false>(a, st);
 }
 
 template <int L, bool INV, bool SHOUP, bool SCALE>
@@ -1037,33 +1024,13 @@ __global__ __launch_bounds__(512) void ntt_r8_kernel(NttArgs<1> a) {
   }
 }
 
-template <bool INV, bool SCALE, bool COL, bool QLO1, bool PF>
-static rg_status launch_r8_pf(const NttArgs<1>& a, hipStream_t st) {
-  const long long ntiles = a.total_sub / 16;
-  if (!PF) {  // one tile per workgroup
-    hipLaunchKernelGGL((ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>), dim3((unsigned)ntiles), dim3(512), 0, st, a);
-    return check_launch("ntt_r8");
-  }
-  static int cap = 0;
-  if (!cap) {  // persistent grid: the resident capacity (RINGO_NTT_WG_PER_CU overrides)
-    int per_cu = 0, dev = 0, cus = 256;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>, 512, 0);
-    const char* e = knob(Knob::NttWgPerCu);
-    if (e) per_cu = atoi(e);
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    cap = (per_cu > 0 ? per_cu : 1) * cus;
-  }
-  const long long grid = ntiles < cap ? ntiles : cap;
-  hipLaunchKernelGGL((ntt_r8_kernel<INV, SCALE, COL, QLO1, PF>), dim3((unsigned)grid), dim3(512), 0, st, a);
-  return check_launch("ntt_r8");
-}
-
+// one tile per workgroup (the persistent prefetching grid, PF = true, measured slower in round 2
+// and is no longer instantiated: tools/experiments/ntt_knob_kernels.patch)
 template <bool INV, bool SCALE, bool COL, bool QLO1>
 static rg_status launch_r8_q(const NttArgs<1>& a, hipStream_t st) {
-  static const int pf = knob(Knob::NttR8Pf) ? atoi(knob(Knob::NttR8Pf)) : 0;
-  return pf ? launch_r8_pf<INV, SCALE, COL, QLO1, true>(a, st)
-                               : launch_r8_pf<INV, SCALE, COL, QLO1, false>(a, st);
+  const long long ntiles = a.total_sub / 16;
+  hipLaunchKernelGGL((ntt_r8_kernel<INV, SCALE, COL, QLO1, false>), dim3((unsigned)ntiles), dim3(512), 0, st, a);
+  return check_launch("ntt_r8");
 }
 
 template <bool INV, bool SCALE, bool COL>
@@ -1071,15 +1038,6 @@ static rg_status launch_r8(const NttArgs<1>& a, hipStream_t st) {
   return a.qlo1 ? launch_r8_q<INV, SCALE, COL, true>(a, st) : launch_r8_q<INV, SCALE, COL, false>(a, st);
 }
 
-// RINGO_NTT_KERNEL=r2 selects the radix-16 pass instead (A/B switch)
-static inline bool use_r8() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = knob(Knob::NttKernel);
-    v = (e && e[0] == 'r' && e[1] == '2') ? 0 : 1;
-  }
-  return v == 1;
-}
 
 }  // namespace rg
 
@@ -1112,24 +1070,21 @@ static rg_status run_tiled(const NttLaunch& p, hipStream_t st) {
       const int logS = p.logN - ps.G0 - ps.P;
       if (RadixOf<L>::value == 4 && ps.P == 8 && (logS == 0 || logS >= 4) && (a.total_sub % 16) == 0) {
         const bool col = logS >= 4;
-        if constexpr (L == 1 && SHOUP) {
-          if (use_r8()) {
-            if (!p.inv)
-              s = col ? launch_r8<false, false, true>(a, st) : launch_r8<false, false, false>(a, st);
-            else if (ps.G0 == 0)
-              s = col ? launch_r8<true, true, true>(a, st) : launch_r8<true, true, false>(a, st);
-            else
-              s = col ? launch_r8<true, false, true>(a, st) : launch_r8<true, false, false>(a, st);
-            RG_TRY(s);
-            continue;
-          }
+        if constexpr (L == 1 && SHOUP) {  // radix-8 rounds (the radix-16 form measured slower)
+          if (!p.inv)
+            s = col ? launch_r8<false, false, true>(a, st) : launch_r8<false, false, false>(a, st);
+          else if (ps.G0 == 0)
+            s = col ? launch_r8<true, true, true>(a, st) : launch_r8<true, true, false>(a, st);
+          else
+            s = col ? launch_r8<true, false, true>(a, st) : launch_r8<true, false, false>(a, st);
+        } else {
+          if (!p.inv)
+            s = dispatch_r2<L, false, SHOUP, false>(col, a, st);
+          else if (ps.G0 == 0)
+            s = dispatch_r2<L, true, SHOUP, true>(col, a, st);
+          else
+            s = dispatch_r2<L, true, SHOUP, false>(col, a, st);
         }
-        if (!p.inv)
-          s = dispatch_r2<L, false, SHOUP, false>(col, a, st);
-        else if (ps.G0 == 0)
-          s = dispatch_r2<L, true, SHOUP, true>(col, a, st);
-        else
-          s = dispatch_r2<L, true, SHOUP, false>(col, a, st);
         RG_TRY(s);
         continue;
       }

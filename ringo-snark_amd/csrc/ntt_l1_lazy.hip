@@ -1,7 +1,7 @@
 // ntt_l1_lazy.hip -- dispatch of the lazy single-word pass kernels (ntt64.hpp) for the shapes
 // they cover: N = 2^16 as two 8-stage passes, q < 2^63 with q mod 2^32 == 1 (the config-2
 // jindo-modulus prime 47104^4 + 1 and every other p - 1 = b^(2^e) with b even).  Other shapes
-// keep the generic kernels of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r8|r2 forces the generic path
+// keep the generic kernels of ntt_kernels.hpp.  RINGO_NTT_KERNEL=r* forces the generic path
 // (experiments build only, common.hpp).
 #include "ntt64.hpp"
 #include "ntt_plan.hpp"

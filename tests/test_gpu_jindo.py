@@ -258,20 +258,17 @@ MAC_SHAPES = [("t14_b1", 16384), ("mult_t8193_b12", 8193), ("t10_b8", 1024)]
 
 
 def test_mac_paths_agree(tmp_path):
-    """The three inner/outer MAC kernels (the MFMA digit MAC, mac3h on the VALU, mac_kernel)
-    produce the same Opening.InCommit and Commitment.Value bit for bit.  The product library
-    (this process) must run the MFMA MAC on both products of every shape; the other two run in
-    child processes on the experiments build with RINGO_JINDO_MAC=h / l (tests/exp_child.py), each
-    checked to have taken the kernel it names.  MSIS ranks J > 16 (examples/mult's 21) take
-    mac_kernel in every mode: there this compares the product's fallback with itself, and
-    test_commit_matches_oracle pins it."""
+    """The two inner/outer MAC kernels (the MFMA digit MAC and mac_kernel) produce the same
+    Opening.InCommit and Commitment.Value bit for bit.  The product library (this process) must
+    run the MFMA MAC on both products of every shape; mac_kernel runs in a child process on the
+    experiments build with RINGO_JINDO_MAC=l (tests/exp_child.py), checked to have taken it.  MSIS
+    ranks J > 16 (examples/mult's 21) take mac_kernel in both: there this compares the product's
+    fallback with itself, and test_commit_matches_oracle pins it."""
     import subprocess
     import sys
 
     def expect(J, mode):
-        if J > 16 or mode == "l":
-            return "generic"
-        return "valu3" if mode == "h" else "mfma"
+        return "generic" if J > 16 or mode == "l" else "mfma"
 
     want = {}
     for name, nv in MAC_SHAPES:
@@ -280,7 +277,7 @@ def test_mac_paths_agree(tmp_path):
         assert prv.mac_kinds() == (expect(P["in_msis"], ""), expect(P["out_msis"], "")), name
         com, op = prv.Commit(make_v(q, nv, seed=5), jindo.Randomness(**make_randomness(P, q, seed=9)))
         want[name] = (op.InCommit.copy(), com.Value.copy())
-    for mode in ("h", "l"):
+    for mode in ("l",):
         out = tmp_path / f"mac_{mode}.npz"
         r = subprocess.run([sys.executable, os.path.join(HERE, "exp_child.py"), "mac", mode, str(out)] +
                            [f"{n}:{nv}" for n, nv in MAC_SHAPES], capture_output=True, text=True, timeout=110)

@@ -1,7 +1,7 @@
 """GPU parity at the configs[4] shape (NewParameters(2^16, 4096): 2 x 58-bit ringQ primes, 2 x
 54-bit ringQOut primes, rows 513, cols 8, inMSIS 16, J = 16, logOutCut 74) -- the shape the
 bench's jindo_commit_2e16 / jindo_evaluate_2e16 lines run -- plus the Ajtai-core entry point
-(rg_jindo_commit_core, prover.go:144-202), the mac3 fold boundary, per-stream scratch and the
+(rg_jindo_commit_core, prover.go:144-202), the MAC's extreme inputs, per-stream scratch and the
 device-resident commit key.  Oracle: oracle/oracle.c (CJindo), bit-exact."""
 import json
 import os
@@ -99,11 +99,11 @@ def test_commit_core_matches_oracle(name):
 
 
 @pytest.mark.parametrize("name", ["t16_b4096", "t10_b8"])
-def test_mac3_fold_boundary(name):
-    """Every commit-key and opening word q - 1: each mac3 accumulator reaches its fold bound
-    (fold period 16 for the 59-bit configs[4] primes: 16 * 2 * 2^59 = 2^64) and the exact
-    128-bit sums their maximum; the InCommit words fed to the outer MAC are whatever rounding
-    gives.  A second prover holds an all-(q-1) key."""
+def test_mac_extreme_inputs(name):
+    """Every commit-key and opening word q - 1: the MFMA MAC's digit diagonals and signed 128-bit
+    fold reach their largest magnitudes (configs[4]: 545 terms x 2^58 x 2^58 = 2^125.1, the bound
+    mac_mfma_nb admits) and the exact sums their maximum; the InCommit words fed to the outer MAC
+    are whatever rounding gives.  A second prover holds an all-(q-1) key."""
     P, q, params, _, _ = _prover(name)
     sh, cks = params.shapes(), params.ck_shapes()
     rng = np.random.default_rng(0)

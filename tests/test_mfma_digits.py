@@ -1,8 +1,7 @@
 """CPU check of the arithmetic behind mac_mfma.hip (the Jindo Ajtai MAC on the matrix cores):
 the key's balanced base-256 digits, byte-reversed and shifted into the A operand of each digit
 diagonal, the opening's bytes offset by 0x80 (read as int8), the per-(lk, j) correction and the
-signed 128-bit fold give (sum_t A[t] B[t]) 2^-64 mod q exactly, as mac3h_kernel / mac_kernel
-compute it (prover.go:149-157, the summed MulCoeffsMontgomeryThenAdd).
+signed 128-bit fold give (sum_t A[t] B[t]) 2^-64 mod q exactly, as mac_kernel computes it (prover.go:149-157, the summed MulCoeffsMontgomeryThenAdd).
 
 This restates the kernel's byte-level formulation in Python (no GPU); the GPU kernel itself is
 checked bit for bit against the oracle by tests/test_gpu_jindo.py (test_mac_paths_agree and the

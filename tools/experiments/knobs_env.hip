@@ -10,10 +10,11 @@ namespace rg {
 static thread_local int t_probe = 0;
 
 const char* knob(Knob k) {
-  static const char* names[] = {"RINGO_NTT_KERNEL", "RINGO_NTT_CHUNK_MB", "RINGO_NTT_PREFETCH",
-                                "RINGO_NTT_WG_PER_CU", "RINGO_NTT_R8_PF", "RINGO_JINDO_PREP",
-                                "RINGO_JINDO_PREP_W", "RINGO_JINDO_MAC", "RINGO_JINDO_SPLIT",
-                                "RINGO_JINDO_EVAL", "RINGO_JINDO_UNI_TRIES"};
+  // (round 6 removed the knobs whose kernels only an A/B run reached: RINGO_NTT_PREFETCH,
+  // RINGO_NTT_WG_PER_CU, RINGO_NTT_R8_PF, RINGO_JINDO_PREP, RINGO_JINDO_PREP_W, RINGO_JINDO_EVAL and
+  // RINGO_JINDO_MAC=h; tools/experiments/jindo_knob_kernels.patch, ntt_knob_kernels.patch)
+  static const char* names[] = {"RINGO_NTT_KERNEL", "RINGO_NTT_CHUNK_MB", "RINGO_JINDO_MAC", "RINGO_JINDO_SPLIT",
+                                "RINGO_JINDO_UNI_TRIES"};
   static_assert(sizeof(names) / sizeof(names[0]) == (size_t)Knob::Count, "knob names");
   const int i = (int)k;
   if (i < 0 || i >= (int)Knob::Count) return nullptr;
