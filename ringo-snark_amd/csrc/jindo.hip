@@ -38,6 +38,7 @@
 #include "ck_crs.hpp"
 #include "common.hpp"
 #include "csprng.hpp"
+#include "digits_dc.hpp"
 #include "csprng_host.hpp"
 #include "field.hpp"
 #include "host_field.hpp"
@@ -149,6 +150,7 @@ struct DigitArgs {
   FieldParams<L> F;
   uint64_t base_inv;  // floor(2^64 / base)
   uint64_t b2, b2_inv;  // base^2 and floor(2^64 / base^2) when base^2 < 2^32, else 0
+  DigitDc dc;           // divide-and-conquer constants (digits_dc.hpp); dc.exp = 0: the loop below
   const uint64_t* v;         // [B][nv][L]
   const uint64_t* last_row;  // [B][cols*slots][L]
   const uint64_t* mask;      // [B][rows][slots][L]
@@ -288,6 +290,12 @@ __global__ __launch_bounds__(256) void digits_kernel(DigitArgs<L> a) {
     for (int l = 0; l < L; ++l) c[l] = 0;
   }
   // base-b digits: exp-1 remainders then the final quotient (encoder.go:125-136)
+  if constexpr (L == 4 || L == 2) {
+    if (a.dc.exp == S.exp) {  // every configs field: by divide and conquer (digits_dc.hpp)
+      dc_digits<L>(c, a.dc, [&](int j, uint32_t dg) { out[j * S.slots + slot] = dg; });
+      return;
+    }
+  }
   uint32_t w[2 * L];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
@@ -2454,6 +2462,10 @@ static rg_status launch_digits(const rg_jindo* J, size_t batch, const uint64_t* 
   const uint64_t b2 = (uint64_t)J->p.base * J->p.base;
   a.b2 = (b2 >> 32) ? 0 : b2;
   a.b2_inv = a.b2 ? (uint64_t)(((unsigned __int128)1 << 64) / b2) : 0;
+  int qbits = 0;
+  for (int l = L - 1; l >= 0 && !qbits; --l)
+    if (J->field.q[l]) qbits = 64 * l + 64 - __builtin_clzll(J->field.q[l]);
+  a.dc = dc_constants((uint64_t)J->p.base, J->p.exp, L, qbits);
   a.v = v;
   a.last_row = last;
   a.mask = mask;

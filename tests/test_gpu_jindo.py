@@ -43,6 +43,45 @@ def test_commit_key_from_crs(name):
         assert (g == np.array(w, dtype=np.uint64)).all()
 
 
+def _edge_v(q, b, exp, n, seed):
+    """v (Montgomery form, R = 2^(64L)) whose canonical values hit the digit split's boundaries
+    (csrc/digits_dc.hpp): 0, q - 1, powers of b and of B4 = b^4 / B8 = b^8 and their neighbours,
+    then seeded random values"""
+    L = (q.bit_length() + 63) // 64
+    R = 1 << (64 * L)
+    vals = [0, 1, q - 1, q - 2]
+    for k in range(exp + 1):
+        vals += [b ** k - 1, b ** k, b ** k + 1, q - b ** k]
+    for m in (1, 2, 3, 7):
+        vals += [m * b ** 4 - 1, m * b ** 4, (q // b ** 8) * b ** 8 - m, m * b ** 8 - 1, m * b ** 8]
+    rng = np.random.default_rng(seed)
+    vals = [x % q for x in vals]
+    vals += [int(rng.integers(0, 1 << 62)) * int(rng.integers(0, 1 << 62)) % q for _ in range(max(0, n - len(vals)))]
+    vals = vals[:n]
+    out = np.zeros((n, L), np.uint64)
+    for i, c in enumerate(vals):
+        m = c * R % q
+        for j in range(L):
+            out[i, j] = (m >> (64 * j)) & ((1 << 64) - 1)
+    return out
+
+
+@pytest.mark.parametrize("name", ["t14_b1", "mult_t8193_b12"])
+def test_commit_digit_edges_match_oracle(name):
+    """Encode's base-b digits of boundary values (divide-and-conquer split on the device) vs the
+    oracle's repeated division, through the whole commit."""
+    P, q, params = _setup(name)
+    prv = jindo.NewProver(params, b"Jindo!")
+    ck = prv.commit_key()
+    nv = min(P["rank"], 400)
+    v = _edge_v(q, P["base"], P["exp"], nv, seed=3)
+    rnd = make_randomness(P, q, seed=17)
+    com, op = prv.Commit(v, jindo.Randomness(**rnd))
+    want = _oracle_commit(P, q, ck, v, rnd)
+    assert (op.Encode == want["enc"]).all(), name
+    assert (com.Value == want["com"]).all(), name
+
+
 @pytest.mark.parametrize("name,nvs", [("t10_b1", [1024, 300, 33, 1]), ("t10_b8", [1024, 129]),
                                       ("mult_t8193_b12", [8193, 700]), ("t14_b1", [16384, 5000])])
 def test_commit_matches_oracle(name, nvs):
