@@ -1883,40 +1883,61 @@ __global__ __launch_bounds__(512) void uniform_whole_kernel(UniArgs<L> a, int* f
   const JShape& S = a.s;
   const long long nl = (long long)S.cols * S.slots, per = nl + (long long)S.rows * S.slots;
   const uint64_t topm = ((uint64_t)a.top_mask << 56) | 0x00FFFFFFFFFFFFFFull;
-  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
-       gid += (long long)gridDim.x * blockDim.x) {
-    long long b, i;
-    if (a.total <= 0xffffffffLL) {
-      b = idx_div((uint32_t)gid, a.d_per);
-      i = gid - b * per;
-    } else {
-      b = gid / per;
-      i = gid % per;
-    }
-    uint64_t* dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
-    if (i == nl - 1) {
-#pragma unroll
-      for (int l = 0; l < L; ++l) dst[l] = 0;
-      continue;
-    }
-    const unsigned long long inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
-    bool done = false;
-    for (int t = 0; t < max_tries; ++t) {
-      uint64_t z[L];
-#pragma unroll
-      for (int h = 0; h < L / 2; ++h) ks_words(LdsKey{key}, inst, (uint64_t)t * (L / 2) + h, lds, z[2 * h], z[2 * h + 1]);
-      z[L - 1] &= topm;  // the last byte's unused top bits (element.go:320-325)
-      if (!geq_q<L>(z, a.F)) {
-#pragma unroll
-        for (int l = 0; l < L; ++l) dst[l] = z[l];
-        done = true;
-        break;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  // One try per iteration, and a lane moves on to its next element (grid-stride) as soon as its
+  // current one is accepted: the wave no longer waits, element by element, for its slowest lane
+  // (a try is accepted with probability q / 2^bitlen(q-1), 0.52 at q255: the most tries among 64
+  // lanes averages ~6 against 1.9 per lane).  Same draws: element i's try t reads the same blocks.
+  long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t* dst = nullptr;
+  unsigned long long inst = 0;
+  int t = 0;
+  auto next = [&]() {  // from gid: the element's destination and instance; skips lastRow's last entry
+    while (gid < a.total) {
+      long long b, i;
+      if (a.total <= 0xffffffffLL) {
+        b = idx_div((uint32_t)gid, a.d_per);
+        i = gid - b * per;
+      } else {
+        b = gid / per;
+        i = gid % per;
       }
-    }
-    if (!done) {
+      dst = i < nl ? a.last_row + (b * nl + i) * L : a.mask + (b * (per - nl) + (i - nl)) * L;
+      if (i != nl - 1) {
+        inst = (a.first_commit + (unsigned long long)b) * (unsigned long long)per + (unsigned long long)i;
+        t = 0;
+        return;
+      }
 #pragma unroll
-      for (int l = 0; l < L; ++l) dst[l] = ~0ull;
-      *flag = 1;
+      for (int l = 0; l < L; ++l) dst[l] = 0;  // genFirstLastRow leaves it zero
+      gid += stride;
+    }
+  };
+  next();
+  static_assert(L % 2 == 0, "whole 16-byte blocks per try");
+  while (gid < a.total) {
+    uint64_t z[L];
+    bool ok = false;
+    if (max_tries > 0) {  // (0: every draw left to the fix-up, the experiments build's test)
+      if constexpr (L >= 4) {
+#pragma unroll
+        for (int h = 0; h < L / 4; ++h)
+          ks_words_x2(LdsKey{key}, inst, (uint64_t)t * (L / 2) + 2 * h, (uint64_t)t * (L / 2) + 2 * h + 1, lds,
+                      z + 4 * h);
+      }
+      if constexpr (L % 4 != 0)
+        ks_words(LdsKey{key}, inst, (uint64_t)t * (L / 2) + (L / 2 - 1), lds, z[L - 2], z[L - 1]);
+      z[L - 1] &= topm;  // the last byte's unused top bits (element.go:320-325)
+      ok = !geq_q<L>(z, a.F);
+    }
+    if (ok || t + 1 >= max_tries) {
+      if (!ok) *flag = 1;
+#pragma unroll
+      for (int l = 0; l < L; ++l) dst[l] = ok ? z[l] : ~0ull;
+      gid += stride;
+      next();
+    } else {
+      ++t;
     }
   }
 }
