@@ -2788,12 +2788,15 @@ static rg_status launch_uniform(const rg_jindo* J, size_t batch, const AesKey& k
   a.total = (long long)batch * ((long long)J->p.cols * J->p.slots + (long long)J->p.rows * J->p.slots);
   a.d_per = make_idxdiv((uint32_t)(J->p.cols * J->p.slots + J->p.rows * J->p.slots));
   const dim3 ug((unsigned)std::min<long long>((a.total + 511) / 512, 1024));
+  // whole-word draws: about 4 elements per lane (the flattened try loop balances lanes only over
+  // several elements), at least one workgroup per CU
+  const dim3 ugw((unsigned)std::max<long long>(std::min<long long>((a.total + 512 * 4 - 1) / (512 * 4), 1024), std::min<long long>((a.total + 511) / 512, 256)));
   if constexpr (L % 2 == 0) {
     if (a.kbytes == 8 * L) {  // whole words: the common draws, then the (practically never) long ones
       const char* kt = knob(Knob::JindoUniTries);  // experiments build: cap the tries (fix-up test)
       const int tries = std::max(0, std::min(1024 / L, kt ? atoi(kt) : 1024 / L));
       RG_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
-      hipLaunchKernelGGL(uniform_whole_kernel<L>, ug, dim3(512), 0, st, a, flag, tries);
+      hipLaunchKernelGGL(uniform_whole_kernel<L>, ugw, dim3(512), 0, st, a, flag, tries);
       RG_TRY(check_launch("jindo uniform (whole words)"));
       hipLaunchKernelGGL(uniform_fix_kernel<L>, ug, dim3(512), 0, st, a, (const int*)flag);
       return check_launch("jindo uniform (long draws)");
