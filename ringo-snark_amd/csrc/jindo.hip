@@ -442,7 +442,7 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
-template <int RK, int LO, int PAT, int SP0 = 0>
+template <int RK, int LO, int PAT, int SP0 = 0, bool LAZY = false>
 __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* roots, uint64_t q, uint64_t q2,
                                            uint32_t t) {
   auto xof = [&](int rho) -> uint32_t {
@@ -462,7 +462,9 @@ __device__ __forceinline__ void prep_round(uint64_t (&e)[8], const ulonglong2* r
       // Harvey with a 4q-wide twiddle product: values in [0, 8q) (ring primes < 2^61), x
       // reduced to [0, 4q), t = y w - Q' q in [0, 4q) with Q' the Shoup quotient less the low
       // cross products (Q - 2 <= Q' <= Q): three 32-bit multiplies for the quotient, not four
-      const uint64_t x = canon_x(e[rho0], q2);  // x >= 4q ? x - 4q : x, on the borrow (q2 = 4q here)
+      // x >= 4q ? x - 4q : x, on the borrow (q2 = 4q here); LAZY (36 q < 2^64): x unreduced, each
+      // stage widens the bound by 4q, [0, 8q) after stage 0 -> [0, 36q) after stage 7
+      const uint64_t x = LAZY ? e[rho0] : canon_x(e[rho0], q2);
       const uint64_t y = e[rho0 + half];
       const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32), p0 = (uint32_t)w.y, p1 = (uint32_t)(w.y >> 32);
       const uint64_t qa = mad64(y1, p1, __umulhi(y1, p0)) + __umulhi(y0, p1);
@@ -487,7 +489,7 @@ __device__ __forceinline__ uint64_t red_signed(long long c, const RnsPrime& P) {
   return c < 0 ? mod_neg(m, P.q) : m;
 }
 
-template <int MINW, bool PAIR1, int WAVES = kPrepWaves>
+template <int MINW, bool PAIR1, int WAVES = kPrepWaves, bool LAZY = false>
 __global__ __launch_bounds__(64 * WAVES, MINW) void prep256_kernel(PrepArgs a) {
   __shared__ uint64_t lds_all[WAVES][2 * 288];
   extern __shared__ ulonglong2 tw_lds[];  // the nq limbs' forward tables (w, w'), [nq][256]: dynamic LDS
@@ -605,24 +607,24 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void prep256_kernel(PrepArgs a) {
       }
     }
     // NTT: H round (stages 1-2; 0 above), H->M, M round (3-5), M->L, L round (6-7), L->H, store
-    prep_round<3, 5, 0, 1>(e, roots, q, q2, t);
+    prep_round<3, 5, 0, 1, LAZY>(e, roots, q, q2, t);
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rH + 36 * y] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) e[y] = lds[rM + 4 * y];
-    prep_round<3, 2, 1>(e, roots, q, q2, t);
+    prep_round<3, 2, 1, 0, LAZY>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
     for (int y = 0; y < 8; ++y) lds[rM + 4 * y + (y >> 1)] = e[y];
     wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 8; ++r) e[r] = lds[rL9 + r];
-    prep_round<2, 0, 2>(e, roots, q, q2, t);
+    prep_round<2, 0, 2, 0, LAZY>(e, roots, q, q2, t);
     wave_lds_fence();
 #pragma unroll
-    for (int r = 0; r < 8; ++r)  // [0, 8q) -> [0, q)
-      lds[rL8 + r] = canon_x(canon_x(canon_x(e[r], q2), 2 * q), q);
+    for (int r = 0; r < 8; ++r)  // [0, 8q) (LAZY: [0, 36q), Shoup by 1) -> [0, q)
+      lds[rL8 + r] = LAZY ? shoup_mul(e[r], 1, P.one_sh, q) : canon_x(canon_x(canon_x(e[r], q2), 2 * q), q);
     wave_lds_fence();
     if (active) {
       uint64_t* o = dst + (long long)limb * 256;
@@ -2704,10 +2706,17 @@ static rg_status prep_launch(rg_jindo* J, size_t batch, size_t nv, const uint32_
     constexpr int kBigWaves = 12;
     // (minimum waves per SIMD 8 or 1 instead of 6, round 2-5's RINGO_JINDO_PREP_W: slower at both
     // configs shapes, removed in round 6)
+    bool lazy = true;  // every ring prime below 2^64 / 36: prep_round skips its x reductions
+    for (int l = 0; l < nq; ++l) lazy = lazy && J->rq[l].q < ~0ull / 36;
     if (nq <= 2 && jobs >= (1LL << 20)) {
-      hipLaunchKernelGGL((prep256_kernel<2, true, kBigWaves>), dim3((unsigned)((jobs + kBigWaves - 1) / kBigWaves)),
-                         dim3(64 * kBigWaves), twl, st, pa);
-    } else if (nq <= 2)
+      const dim3 gb((unsigned)((jobs + kBigWaves - 1) / kBigWaves)), bb(64 * kBigWaves);
+      if (lazy)
+        hipLaunchKernelGGL((prep256_kernel<2, true, kBigWaves, true>), gb, bb, twl, st, pa);
+      else
+        hipLaunchKernelGGL((prep256_kernel<2, true, kBigWaves>), gb, bb, twl, st, pa);
+    } else if (nq <= 2 && lazy)
+      hipLaunchKernelGGL((prep256_kernel<6, true, kPrepWaves, true>), g, b, twl, st, pa);
+    else if (nq <= 2)
       hipLaunchKernelGGL((prep256_kernel<6, true>), g, b, twl, st, pa);
     else
       hipLaunchKernelGGL((prep256_kernel<6, false>), g, b, twl, st, pa);
