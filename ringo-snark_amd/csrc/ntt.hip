@@ -4,6 +4,7 @@
 // ntt_l1.hip / ntt_l2.hip / ntt_l4.hip / ntt_lwide.hip.
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "common.hpp"
@@ -28,6 +29,7 @@ struct rg_ntt {
   rg::DevBuf d_tw, d_twinv;                     // kernel format
   std::vector<rg::PassDesc> passes;             // forward order
   uint64_t nsc[16], nsc_sh, w1n[16], w1n_sh;
+  std::unique_ptr<rg::Aux> aux;  // L = 4: helper stream of ntt256_run's split (ntt_l4_fast.hip)
 };
 
 namespace rg {
@@ -225,6 +227,12 @@ static rg_status finalize(rg_ntt* t) {
     memcpy(t->w1n, w1n, 8 * L);
     t->nsc_sh = t->w1n_sh = 0;
   }
+  if (L == 4 && (t->logN == 15 || t->logN == 16)) {
+    t->aux.reset(new Aux());
+    RG_HIP(hipStreamCreateWithFlags(&t->aux->s, hipStreamNonBlocking));
+    RG_HIP(hipEventCreateWithFlags(&t->aux->fork, hipEventDisableTiming));
+    RG_HIP(hipEventCreateWithFlags(&t->aux->join, hipEventDisableTiming));
+  }
   return RG_OK;
 }
 
@@ -248,6 +256,7 @@ static rg_status run(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t 
   p.passes = t->passes.data();
   p.npasses = (int)t->passes.size();
   p.batch = batch;
+  p.aux = t->aux.get();
   switch (t->f.L) {
     case 1: {
       bool done = false;

@@ -25,17 +25,47 @@ static rg_status launch256(const Ntt256Args& a, size_t polys, hipStream_t st) {
 }
 
 template <int LOGN>
-static rg_status run_passes(Ntt256Args a, const NttLaunch& p, hipStream_t st) {
+static rg_status run_passes(Ntt256Args a, const NttLaunch& p, size_t polys, hipStream_t st) {
   if (!p.inv) {
-    RG_TRY((launch256<false, true, false, false, LOGN>(a, p.batch, st)));
+    RG_TRY((launch256<false, true, false, false, LOGN>(a, polys, st)));
     a.in = a.out;
-    RG_TRY((launch256<false, false, false, true, LOGN>(a, p.batch, st)));
+    RG_TRY((launch256<false, false, false, true, LOGN>(a, polys, st)));
   } else {
-    RG_TRY((launch256<true, false, false, false, LOGN>(a, p.batch, st)));
+    RG_TRY((launch256<true, false, false, false, LOGN>(a, polys, st)));
     a.in = a.out;
-    RG_TRY((launch256<true, true, true, true, LOGN>(a, p.batch, st)));
+    RG_TRY((launch256<true, true, true, true, LOGN>(a, polys, st)));
   }
   return RG_OK;
+}
+
+// The batch as two halves, the first on the caller's stream and the second on the plan's helper
+// stream: each pass is ~2.7 rounds of workgroups (3 per SIMD resident), and the halves' passes
+// fill each other's last round (configs[3] fwd+inv: 182.5 -> 187.3 K NTT/s; four quarters
+// alternating measured 160 K, the headline ntt16_pass split lost 1.5%: profiles/r06r_ntt_split.txt)
+template <int LOGN>
+static rg_status run_split(Ntt256Args a, const NttLaunch& p, hipStream_t st) {
+  Aux* x = p.aux;
+  if (!x || p.batch < 8 || measure_probe() == 5) return run_passes<LOGN>(a, p, p.batch, st);
+  const size_t N = (size_t)1 << LOGN;
+  const size_t h = (p.batch / 2 + 3) & ~(size_t)3;  // the ROW passes' RP tiles take 4 polys
+  Ntt256Args b = a;
+  a.total_sub = (long long)(h * (N >> 8));
+  b.total_sub = (long long)((p.batch - h) * (N >> 8));
+  b.in += h * N * 4;
+  b.out += h * N * 4;
+  std::lock_guard<std::mutex> lk(x->mu);
+  RG_HIP(hipEventRecord(x->fork, st));
+  RG_HIP(hipStreamWaitEvent(x->s, x->fork, 0));
+  rg_status s = run_passes<LOGN>(a, p, h, st);
+  if (s == RG_OK) s = run_passes<LOGN>(b, p, p.batch - h, x->s);
+  // joined on every path, so the caller's stream orders whatever was queued on the helper
+  const hipError_t j[2] = {hipEventRecord(x->join, x->s), hipStreamWaitEvent(st, x->join, 0)};
+  for (hipError_t e : j)
+    if (e != hipSuccess && s == RG_OK) {
+      set_last_error(std::string("ntt256: joining the helper stream: ") + hipGetErrorString(e));
+      s = RG_ERR_DEVICE;
+    }
+  return s;
 }
 
 // N = 2^16 (passes 8 + 8) and N = 2^15 (7 + 8: the Buckler witness rank of the bench)
@@ -65,7 +95,7 @@ rg_status ntt256_run(const NttLaunch& p, hipStream_t st, bool* handled) {
   a.total_sub = (long long)(p.batch * (N >> 8));
   a.in = p.in;
   a.out = p.out;
-  return p.logN == 16 ? run_passes<16>(a, p, st) : run_passes<15>(a, p, st);
+  return p.logN == 16 ? run_split<16>(a, p, st) : run_split<15>(a, p, st);
 }
 
 }  // namespace rg

@@ -1,5 +1,7 @@
 // ntt_plan.hpp -- what ntt.hip hands to the per-limb-count kernel translation units.
 #pragma once
+#include <mutex>
+
 #include "common.hpp"
 
 namespace rg {
@@ -25,6 +27,21 @@ struct NttLaunch {
   const PassDesc* passes;  // forward order
   int npasses;
   size_t batch;
+  // the plan's helper stream for ntt256_run's two-half split (null: single stream); the mutex
+  // serialises the fork/join enqueue of concurrent callers, which share the events
+  struct Aux* aux = nullptr;
+};
+
+// a helper stream and the two events that fork it from and join it back to the caller's stream
+struct Aux {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+  ~Aux() {
+    if (s) (void)hipStreamDestroy(s);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+  }
 };
 
 // the field and kind of a plan (for the operators built on it: buckler.hip)

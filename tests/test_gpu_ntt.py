@@ -210,6 +210,51 @@ def test_ntt_2e16_q255_bench_batch_spot_check(fields):
     assert torch.equal(x, ref)
 
 
+@pytest.mark.parametrize("logn", [16, 15])
+def test_ntt_q255_split_halves_match_oracle(fields, logn):
+    """From 8 polynomials up ntt256_run runs the batch as two halves, the second on the plan's
+    helper stream (ntt_l4_fast.hip run_split): batches 8 (4 + 4, both halves on the same-row-of-4
+    ROW tiling), 9 (4 + 5: the second half on the 4-rows-of-one-poly tiling) and 14 (8 + 6), on a
+    side stream, out of place then in place, every polynomial against the C oracle.  Then two
+    streams share the plan with interleaved transforms (the fork/join events are per plan)."""
+    import torch
+    q = fields["jindo_zp"]
+    N = 1 << logn
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    T = ringo.CyclotomicTransformer(F, N)
+    tw, twi, ninv = cf.tables(N)
+    side = torch.cuda.Stream()
+    for B in (8, 9, 14):
+        rng = np.random.default_rng(1000 + B + logn)
+        a = F.random(B * N, rng).reshape(B, N, F.L)
+        x = torch.from_numpy(a.view(np.int64).reshape(-1).copy()).cuda()
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        T.fwd_dev(y, x, B, stream=side)
+        T.inv_dev(x, y, B, stream=side)  # y -> x: ordered behind the forward's helper half
+        side.synchronize()
+        assert (y.cpu().numpy().view(np.uint64).reshape(B, N, F.L) == cf.ntt_fwd(a, tw)).all(), B
+        assert (x.cpu().numpy().view(np.uint64).reshape(B, N, F.L) == a).all(), B
+        T.inv_dev(x, x, B, stream=side)
+        side.synchronize()
+        assert (x.cpu().numpy().view(np.uint64).reshape(B, N, F.L) == cf.ntt_inv(a, twi, ninv)).all(), B
+    B = 12
+    rng = np.random.default_rng(77 + logn)
+    a = F.random(2 * B * N, rng).reshape(2, B, N, F.L)
+    xs = [torch.from_numpy(a[i].view(np.int64).reshape(-1).copy()).cuda() for i in range(2)]
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for i in range(2):
+            T.fwd_dev(xs[i], xs[i], B, stream=sts[i])
+        for i in range(2):
+            T.inv_dev(xs[i], xs[i], B, stream=sts[i])
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert (xs[i].cpu().numpy().view(np.uint64).reshape(B, N, F.L) == a[i]).all(), i
+
+
 @pytest.mark.parametrize("name,B", [("zp440", 32), ("zp880", 16)])
 def test_ntt_2e16_wide_bench_batch_spot_check(fields, name, B):
     """The wide Buckler fields at the batch bench.py's wide_ntt_* lines time (zp440 x 32,
