@@ -37,6 +37,14 @@ CONFIGS = {
     "t16_b4096": (Q255, 1 << 16, 4096),  # configs[4]
     "mult_t8193_b12": (Q128, 8193, 12),  # configs[0] (examples/mult at rank 2^12)
 }
+# the other fields of the zp package as Jindo fields (buckler/compile.go:178 commits Buckler
+# witnesses with jindo.NewParameters[E] of the Buckler field): every encode exponent 4 .. 64, field
+# limbs 1, 2, 4, 7, 14, one- and two-prime rings, both sides of prep256's lazy-butterfly bound
+_FIELDS = json.load(open(os.path.join(HERE, "fields.json")))
+for _name, _f, _tn, _b in (("p63_t10_b2", "p63", 1 << 10, 2), ("zp110_t10_b1", "zp110", 1 << 10, 1),
+                           ("zp220_t10_b1", "zp220", 1 << 10, 1), ("zp440_t10_b2", "zp440", 1 << 10, 2),
+                           ("zp880_t10_b1", "zp880", 1 << 10, 1)):
+    CONFIGS[_name] = (int(_FIELDS[_f]["q_hex"], 16), _tn, _b)
 
 
 def digest(a):

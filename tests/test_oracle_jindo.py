@@ -40,7 +40,11 @@ def test_params_match_survey_table():
             assert pyref.is_prime(q) and (q - 1) % (2 * P["d"]) == 0
 
 
-@pytest.mark.parametrize("name,nv", [("t10_b1", 1024), ("t10_b1", 300), ("t10_b8", 700), ("mult_t8193_b12", 1500)])
+@pytest.mark.parametrize("name,nv", [("t10_b1", 1024), ("t10_b1", 300), ("t10_b8", 700), ("mult_t8193_b12", 1500),
+                                     # the zp package's other fields as Jindo fields (exp 4 .. 64,
+                                     # limbs 1 .. 14; buckler/compile.go:178)
+                                     ("p63_t10_b2", 1019), ("zp110_t10_b1", 1019), ("zp220_t10_b1", 1019),
+                                     ("zp440_t10_b2", 1019), ("zp880_t10_b1", 1019)])
 def test_c_commit_equals_bigint_commit(name, nv):
     P = PARAMS[name]
     q = int(P["field_q_hex"], 16)
