@@ -53,7 +53,11 @@ def _same(r, want):
     assert r.ok == want["ok"]
 
 
-@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "t14_b1", "mult_t8193_b12"])
+# the zp package's other fields as Jindo fields (test_gpu_jindo_fields.py)
+FIELDS = ["p63_t10_b2", "zp110_t10_b1", "zp220_t10_b1", "zp440_t10_b2", "zp880_t10_b1"]
+
+
+@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "t14_b1", "mult_t8193_b12"] + FIELDS)
 def test_verify_matches_oracle(name):
     P, fq, params, vrf, ck, pr = _setup(name)
     want = oracle_verify(P, fq, ck, pr)
@@ -61,7 +65,7 @@ def test_verify_matches_oracle(name):
     _same(_gpu_verify(vrf, pr), want)
 
 
-@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "mult_t8193_b12"])
+@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "mult_t8193_b12", "p63_t10_b2", "zp880_t10_b1"])
 @pytest.mark.parametrize("what", ["pf_enc", "pf_incom", "y", "pf_partial", "pf_mlwe", "com"])
 def test_tampered_verify_matches_oracle(name, what):
     P, fq, params, vrf, ck, pr = _setup(name)
@@ -75,7 +79,7 @@ def test_tampered_verify_matches_oracle(name, what):
     _same(_gpu_verify(vrf, bad), want)
 
 
-@pytest.mark.parametrize("name", ["t10_b1", "t10_b8"])
+@pytest.mark.parametrize("name", ["t10_b1", "t10_b8"] + FIELDS)
 def test_jindo_flow_on_gpu(name):
     """TestJindo (jindo_test.go:26-52) on the device: Commit with the device samplers, Evaluate's
     MACs on the device (challenges from encodeChallengeTo of random bytes; leftVec / rightVec /
