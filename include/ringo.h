@@ -91,7 +91,9 @@ int rg_ntt_rank(const rg_ntt* t); /* Rank() (ntt.go:139,469) */
 /* Copy the tables out (Montgomery, [rank][L] each + one element). */
 rg_status rg_ntt_tables(const rg_ntt* t, uint64_t* tw, uint64_t* tw_inv, uint64_t* rank_inv);
 
-/* FwdNTTTo(vOut, v) (ntt.go:98-115,206-223) on `batch` polys: natural -> bit-reversed. */
+/* FwdNTTTo(vOut, v) (ntt.go:98-115,206-223) on `batch` polys: natural -> bit-reversed.
+ * The _dev forms order all their work on `stream`; a 4-limb plan at rank 2^15 / 2^16 runs half of a
+ * batch of 8+ on a helper stream of its own, forked from and joined back into `stream`. */
 rg_status rg_ntt_fwd(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t batch);
 rg_status rg_ntt_fwd_dev(const rg_ntt* t, uint64_t* d_out, const uint64_t* d_in, size_t batch, void* stream);
 /* InvNTTTo(vOut, v) (ntt.go:118-136,226-244): bit-reversed -> natural, times rank^-1. */
