@@ -73,10 +73,21 @@ def _shapes():
     return sorted(seen.items(), key=lambda x: x[1])
 
 
+# the BASELINE configs' fields (q255: configs[2]-[4], examples/mult: configs[0]) must take the fast
+# path; the zp package's other fields (exp 4 .. 64 as Buckler's Jindo fields) keep the device's
+# general long division, pinned by tests/test_gpu_jindo_fields.py
+CONFIG_BASES = {60272, 60256}
+
+
 @pytest.mark.parametrize("shape", _shapes(), ids=lambda s: s[1])
 def test_digits_dc_matches_integers(lib, shape):
     (b, exp, L, q), _ = shape
-    assert lib.dc_check(b, exp, L, q.bit_length()) == exp  # every configs field takes the fast path
+    got = lib.dc_check(b, exp, L, q.bit_length())
+    if b in CONFIG_BASES:
+        assert got == exp  # every configs field takes the fast path
+    assert got in (0, exp)
+    if got == 0:
+        return
     B2, B4 = b * b, b ** 4
     vals = {0, 1, q - 1, q - 2, b - 1, b, B2 - 1, B2, B4 - 1, B4, B4 + 1}
     for k in range(exp + 2):
