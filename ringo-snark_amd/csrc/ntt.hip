@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "common.hpp"
@@ -30,6 +31,7 @@ struct rg_ntt {
   std::vector<rg::PassDesc> passes;             // forward order
   uint64_t nsc[16], nsc_sh, w1n[16], w1n_sh;
   std::unique_ptr<rg::Aux> aux;  // L = 4: helper stream of ntt256_run's split (ntt_l4_fast.hip)
+  int device = 0;                // the tables and the helper stream live on this device
 };
 
 namespace rg {
@@ -132,6 +134,7 @@ static rg_status build_tables(rg_ntt* t) {
 
 static rg_status finalize(rg_ntt* t) {
   const int N = t->N, L = t->f.L;
+  RG_HIP(hipGetDevice(&t->device));
   HostField H(&t->f);
   // pass plan: tiled passes of P in [kMinTiledP, pmax] for L <= 4; per-stage otherwise
   const int pm = pmax_of(L);
@@ -238,6 +241,12 @@ static rg_status finalize(rg_ntt* t) {
 
 static rg_status run(const rg_ntt* t, uint64_t* out, const uint64_t* in, size_t batch, bool inv, hipStream_t st) {
   if (batch == 0) return RG_OK;
+  int cur = -1;
+  RG_HIP(hipGetDevice(&cur));
+  if (cur != t->device) {
+    set_last_error("rg_ntt plan used on device " + std::to_string(cur) + ", created on " + std::to_string(t->device));
+    return RG_ERR_INVALID;
+  }
   NttLaunch p;
   p.in = in;
   p.out = out;
