@@ -60,6 +60,34 @@ def test_encode_dev_batch(fields, key, batch):
             assert (got[b] == want).all(), b
 
 
+def test_encode_dev_batch_q255_split(fields):
+    """The witness rank at the Jindo default prime with a batch of 9: the batched cyclic InvNTT at
+    rank 2^15 runs as two halves (4 + 5 polynomials) on the caller's stream and the plan's helper
+    stream (ntt_l4_fast.hip run_split).  Witnesses 0, 4 (the first half's last) and 8 against the
+    oracle, with and without the random coefficient."""
+    import torch
+    q = fields["jindo_zp"]
+    F = ringo.Field(q)
+    cf = co.CField(q)
+    L = F.L
+    rank, emb, batch = 1 << 15, 1 << 16, 9
+    rng = np.random.default_rng(915)
+    enc = buckler.NewEncoder(F, rank, emb)
+    v = _rand(F, batch * rank, rng).reshape(batch, rank, L)
+    r = _rand(F, batch, rng)
+    dv = torch.from_numpy(v.view(np.int64)).cuda()
+    dr = torch.from_numpy(r.view(np.int64)).cuda()
+    dout = torch.full((batch, emb, L), -1, dtype=torch.int64, device="cuda")
+    scr = torch.empty(max(1, enc.scratch_bytes(batch) // 8), dtype=torch.int64, device="cuda")
+    for rand in (None, dr):
+        enc.encode_dev(dout, dv, batch, d_rand=rand, d_scratch=scr)
+        torch.cuda.synchronize()
+        got = dout.cpu().numpy().view(np.uint64)
+        for b in (0, 4, 8):
+            want = cf.buckler_encode(v[b], emb, rnd=None if rand is None else r[b])
+            assert (got[b] == want).all(), b
+
+
 def test_encode_panics(fields):
     F = ringo.Field(fields["p63"])
     enc = buckler.NewEncoder(F, 64, 64)
