@@ -79,7 +79,7 @@ def test_tampered_verify_matches_oracle(name, what):
     _same(_gpu_verify(vrf, bad), want)
 
 
-@pytest.mark.parametrize("name", ["t10_b1", "t10_b8"] + FIELDS)
+@pytest.mark.parametrize("name", ["t10_b1", "t10_b8", "t14_b1", "mult_t8193_b12"] + FIELDS)
 def test_jindo_flow_on_gpu(name):
     """TestJindo (jindo_test.go:26-52) on the device: Commit with the device samplers, Evaluate's
     MACs on the device (challenges from encodeChallengeTo of random bytes; leftVec / rightVec /

@@ -17,7 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PARAMS = json.load(open(os.path.join(HERE, "golden", "jindo_params.json")))
 
 
-@pytest.fixture(scope="module", params=["t10_b1", "t10_b8"])
+# jindo_test sizes, plus the zp package's widest and narrowest fields as Jindo fields
+@pytest.fixture(scope="module", params=["t10_b1", "t10_b8", "p63_t10_b2", "zp880_t10_b1"])
 def proof(request):
     name = request.param
     P = PARAMS[name]
@@ -42,11 +43,17 @@ def test_tampered_proof_rejected(proof, what):
     bad = dict(pr)
     bad[what] = pr[what].copy()
     flat = bad[what].reshape(-1)
-    flat[3] = (int(flat[3]) + 1) % (1 << 62)
+    i = min(3, flat.size - 1)
+    flat[i] = (int(flat[i]) + 1) % (1 << 62)
     r = oracle_verify(P, fq, ck, bad)
     assert not r["ok"], (name, what)
-    want_fail = {"pf_enc": 1, "pf_incom": 0, "y": 3, "pf_partial": 2}[what]
-    assert not r["flags"][want_fail], (name, what, r["flags"])
+    assert not all(r["flags"]), (name, what, r["flags"])
+    # the check that must catch it, at the jindo_test sizes.  (At zp880, exp 64, ChallengeBound is
+    # min(b, 2^(120/64)) / 2 = 1 (params.go:358-360), so encodeChallengeTo (utils.go:21-46) gives
+    # all-zero challenges and a changed Partial word passes verifyConsistency; verifyEval rejects it.)
+    if name.startswith("t10_"):
+        want_fail = {"pf_enc": 1, "pf_incom": 0, "y": 3, "pf_partial": 2}[what]
+        assert not r["flags"][want_fail], (name, what, r["flags"])
 
 
 def test_norm_decision_is_exact():
