@@ -43,7 +43,8 @@ CONFIGS = {
 _FIELDS = json.load(open(os.path.join(HERE, "fields.json")))
 for _name, _f, _tn, _b in (("p63_t10_b2", "p63", 1 << 10, 2), ("zp110_t10_b1", "zp110", 1 << 10, 1),
                            ("zp220_t10_b1", "zp220", 1 << 10, 1), ("zp440_t10_b2", "zp440", 1 << 10, 2),
-                           ("zp880_t10_b1", "zp880", 1 << 10, 1)):
+                           ("zp880_t10_b1", "zp880", 1 << 10, 1), ("zp440_t14_b1", "zp440", 1 << 14, 1),
+                           ("zp880_t14_b1", "zp880", 1 << 14, 1)):
     CONFIGS[_name] = (int(_FIELDS[_f]["q_hex"], 16), _tn, _b)
 
 

@@ -2,7 +2,8 @@
 buckler/compile.go:178 hands to jindo.NewParameters[E]): p63 (exp 4, 1 limb, 64 slots), zp110
 (exp 8, 2 limbs), zp220 (exp 16, 4 limbs), zp440 (exp 32, 7 limbs, one 59.x-bit ring prime, above
 prep256's lazy-butterfly bound 2^64/36) and zp880 (exp 64, 14 limbs, 4 slots, one 58-bit ring
-prime, below it).  Shapes: tests/golden/jindo_params.json (restated NewParameters at targetN 2^10;
+prime, below it), at targetN 2^10 and, for zp440 / zp880, 2^14.  Shapes:
+tests/golden/jindo_params.json (restated NewParameters;
 test_oracle_jindo.py pins the C oracle against the big-int restatement on the same shapes).
 
 Per shape: the CRS commit key; Commit with injected randomness, full and ragged v, every output of
@@ -25,7 +26,9 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 PARAMS = json.load(open(os.path.join(HERE, "golden", "jindo_params.json")))
 SD_KEYS = jindo.STDDEV_KEYS
-NAMES = ["p63_t10_b2", "zp110_t10_b1", "zp220_t10_b1", "zp440_t10_b2", "zp880_t10_b1"]
+# targetN 2^14 adds larger grids: zp880's 60-bit ring prime (the generic MAC, prime >= 2^60) and
+# zp440's two 31-bit primes
+NAMES = ["p63_t10_b2", "zp110_t10_b1", "zp220_t10_b1", "zp440_t10_b2", "zp880_t10_b1", "zp440_t14_b1", "zp880_t14_b1"]
 
 
 def _setup(name):
